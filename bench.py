@@ -1,0 +1,217 @@
+"""Headline benchmark: Orpheus-3B bf16 TTS, audio-sec / wall-sec (RTF) + p50 first audio.
+
+Workload (BASELINE.json configs[1]): one utterance per step per GPU — a "Hello world"-sized
+prompt (voice-framed, synthetic tokenizer), prefill, 1200 greedy decode steps
+(engine_class.py:103 max_tokens) with repetition penalty 1.1 on hipGraph-captured steps,
+the reference window schedule, and SNAC 24 kHz windows on a second HIP stream.  Weights are
+seeded synthetic Orpheus-3B shapes (no checkpoints offline); since random weights never
+speak, the SNAC schedule consumes a seeded synthetic audio-token stream injected at the id
+level while the LLM still decodes every step.  Multi-GPU: one process per
+GPU, independent utterances per rank (batch-sharded streams, no data-path collective),
+max-over-ranks time, ``scaling: weak``.
+
+    python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "audio-sec/wall-sec (RTF) + p50 first-chunk latency, Orpheus-3B bf16"
+PEAK_HBM_GBS = 8000.0
+MAX_TOKENS = 1200
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--max-tokens", type=int, default=MAX_TOKENS)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=24)
+    return p.parse_args()
+
+
+def synthetic_audio_ids(n, seed):
+    import numpy as np
+    from project_morpheus_amd.config import AUDIO_CODE_BASE
+    rng = np.random.default_rng(seed)
+    codes = rng.integers(1, 4096, size=n)
+    return [int(AUDIO_CODE_BASE + 4096 * (i % 7) + c) for i, c in enumerate(codes)]
+
+
+def cpu_baseline(cfg, prompt, n_decode=6):
+    """Oracle (torch fp32, all host threads) on a bounded sample of the same workload:
+    prefill of the same prompt + ``n_decode`` decode steps of the full 28-layer model, and
+    two 7-frame SNAC windows; extrapolated to RTF for the 1200-token utterance."""
+    import torch
+
+    from oracle import llama_ref as L
+    from oracle import snac_ref
+    from project_morpheus_amd.weights import llm_shapes, synthetic_snac_weights
+
+    rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                     kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
+    # values do not change fp32 CPU matmul speed: fill fast instead of sampling 3.3 G normals
+    w = {k: torch.full(s, 0.01, dtype=torch.float32) for k, s in llm_shapes(cfg).items()}
+    ref = L.LlamaRef(rc, w, max_pos=len(prompt) + n_decode + 8)
+    t0 = time.perf_counter()
+    ref.forward(prompt, [0] * len(prompt), list(range(len(prompt))))
+    t_prefill = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(n_decode):
+        ref.forward([5], [0], [len(prompt) + i])
+    t_tok = (time.perf_counter() - t0) / n_decode
+    sw = synthetic_snac_weights()
+    codes = [[1] * 7, [2] * 14, [3] * 28]
+    t0 = time.perf_counter()
+    for _ in range(2):
+        snac_ref.decode(sw, *codes)
+    t_win = (time.perf_counter() - t0) / 2
+    from project_morpheus_amd.schedule import WindowScheduler
+    n = MAX_TOKENS
+    ws = WindowScheduler()
+    windows = sum(len(ws.push(1 + i % 4000)) for i in range(n)) + len(ws.flush())
+    wall = t_prefill + n * t_tok + windows * t_win
+    audio = (windows - 1) * 2048 / 24000.0  # the first 1-frame window emits nothing
+    return {"value": round(audio / wall, 5), "unit": "audio-sec/wall-sec",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": (f"oracle/llama_ref fp32 Orpheus-3B: prefill {len(prompt)} ids "
+                       f"({t_prefill:.2f}s) + {n_decode} decode steps ({t_tok*1e3:.0f} ms/step) "
+                       f"+ 2 SNAC 7-frame windows ({t_win*1e3:.0f} ms each), extrapolated to "
+                       f"{n} tokens / {windows} windows"),
+            "tok_per_s": round(1.0 / t_tok, 3)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from project_morpheus_amd import config as C
+    from project_morpheus_amd import inference as I
+    from project_morpheus_amd.engine import (LlmEngine, SnacDecoder, Synthesizer,
+                                             UtteranceStats)
+    from project_morpheus_amd.tokenizer import Tokenizer
+    from project_morpheus_amd.weights import synthetic_llm_weights, synthetic_snac_weights
+
+    cfg = C.OrpheusConfig()
+    w = synthetic_llm_weights(cfg, seed=0, device=f"cuda:{local}")
+    llm = LlmEngine(cfg, w, device=local, max_slots=1, max_pos=2048, max_batch=1,
+                    max_prefill=256)
+    del w
+    torch.cuda.empty_cache()
+    snac = SnacDecoder(synthetic_snac_weights(), device=local)
+    syn = Synthesizer(llm, snac, depth=3, seed=rank)
+    tok = Tokenizer(None)
+    prompt = I.prompt_ids(tok.encode("tara: Hello world"))
+    inject = synthetic_audio_ids(args.max_tokens, seed=2 + rank)
+
+    def utterance():
+        st = UtteranceStats()
+        for _ in syn.run(prompt, args.max_tokens, 1.1, stop_ids=(), inject_ids=inject, stats=st):
+            pass
+        return st
+
+    for _ in range(args.warmup):
+        utterance()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [utterance() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    audio = sum(s.audio_seconds for s in stats)
+    firsts = [s.first_audio_ms for s in stats]
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        a = torch.tensor([audio], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM)
+        elapsed, audio = float(t.item()), float(a.item())
+        fl = [None] * world
+        dist.all_gather_object(fl, firsts)
+        firsts = [x for r in fl for x in r]
+
+    # ---- roofline of the dominant kernel (gate/up GEMV: 2*ffn*hidden bf16 per launch) ----
+    st = syn.stream
+    llm.prefill(0, 0, prompt, 1.1, st)
+    for _ in range(3):
+        llm.decode(1, 1.1, st)
+    ms_sum, n_launch = 0.0, 0
+    for _ in range(args.profile_steps):
+        m, n = llm.decode_profiled(1, 1.1, st)
+        ms_sum += m
+        n_launch += n
+    gu_ms = ms_sum / max(1, n_launch)
+    gu_bytes = 2 * cfg.ffn * cfg.hidden * 2
+    gu_gbs = gu_bytes / (gu_ms * 1e-3) / 1e9
+    # pure decode step (graph replay, no SNAC) against the whole-step byte roofline
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n_rep = 50
+    ev0.record(st)
+    for _ in range(n_rep):
+        llm.decode(1, 1.1, st)
+    ev1.record(st)
+    ev1.synchronize()
+    step_ms = ev0.elapsed_time(ev1) / n_rep
+    pos = len(prompt) + 3 + args.profile_steps + n_rep
+    step_bytes = cfg.step_weight_bytes() + pos * cfg.kv_bytes_per_position()
+    llm.release_row(0, st)
+    st.synchronize()
+
+    if rank == 0:
+        steps_audio = audio
+        value = steps_audio / elapsed
+        res = {
+            "metric": METRIC, "value": round(value, 4), "unit": "audio-sec/wall-sec",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": "configs[1]: Orpheus-3B bf16 single stream per GPU, "
+                                   "SNAC 24 kHz, greedy + rep-penalty 1.1, hipGraph decode step",
+                       "model": "orpheus-3b (synthetic weights)", "global_batch": world,
+                       "seq_len": len(prompt) + args.max_tokens, "prompt_ids": len(prompt),
+                       "max_tokens": args.max_tokens, "parallelism": f"streams{world}"},
+            "p50_first_audio_ms": round(statistics.median(firsts), 2),
+            "audio_seconds": round(audio, 3),
+            "decode_step_ms": round(step_ms, 4),
+            "decode_tok_per_s": round(1e3 / step_ms, 1),
+            "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),
+                              "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4)},
+            "roofline": {"kernel": "gemv_kernel<1,2,EPI_SILU,NORM> (gate/up + SiLU*up)",
+                         "bound": "hbm", "achieved": round(gu_gbs, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
+                         "avg_launch_us": round(gu_ms * 1e3, 3), "bytes_per_launch": gu_bytes,
+                         "traffic": None},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg, prompt)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

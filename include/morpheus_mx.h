@@ -1,0 +1,112 @@
+/*
+ * morpheus_mx.h — C ABI of libmorpheus_mx.so, the MI355X-native Orpheus TTS hot path.
+ *
+ * Drop-in boundary for the reference's L0 arithmetic.  The reference has
+ * no native code of its own; these entry points replace the third-party engines it binds:
+ *
+ *   mx_llm_*   replaces the Orpheus decoder loop's LLM engine:
+ *                vLLM AsyncLLMEngine.generate  Orpheus-TTS/orpheus_tts_pypi/orpheus_tts/engine_class.py:117
+ *                (SamplingParams engine_class.py:106-112), llama.cpp Llama(...)/text_to_speech
+ *                Morpheus_Client/tts_engine/llama_local.py:42-52,77, and the remote
+ *                /v1/completions stream Morpheus_Client/tts_engine/remote_backend.py:64-117.
+ *   mx_snac_*  replaces snac.SNAC.decode(codes) + slice + PCM16 in convert_to_audio
+ *                Morpheus_Client/tts_engine/speechpipe.py:76-129 (model load :41-49).
+ *
+ * Conventions: return 0 on success, a negative code on error (message via *_last_error);
+ * no exceptions cross the ABI.  All device I/O pointers are caller-owned device memory (or
+ * host-mapped memory from mx_host_alloc); weights passed to *_set_weight are copied and
+ * packed into context-owned storage.  Streams are hipStream_t passed as void*.  One context
+ * per (GPU, host thread); contexts are not re-entrant.  The host engine calls these from
+ * its own thread (never from the asyncio event loop), mirroring llama_local.py:79.
+ */
+#ifndef MORPHEUS_MX_H
+#define MORPHEUS_MX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_OK 0
+#define MX_ERR_ARG (-1)
+#define MX_ERR_HIP (-2)
+#define MX_ERR_STATE (-3)
+#define MX_ERR_OOM (-4)
+
+#define MX_DTYPE_F32 0
+#define MX_DTYPE_BF16 1
+
+typedef struct mx_llm mx_llm;
+typedef struct mx_snac mx_snac;
+
+/* Llama-3 decoder shape (Orpheus-3B: 3072/28/24/8/128/8192/156940), limits and eps. */
+typedef struct mx_llm_config {
+  int32_t hidden, layers, heads, kv_heads, head_dim, ffn, vocab;
+  int32_t max_slots;    /* concurrent utterance streams (KV slots) */
+  int32_t max_pos;      /* positions per slot (n_ctx, llama_local.py:45) */
+  int32_t max_batch;    /* decode rows per step */
+  int32_t max_prefill;  /* prompt tokens per prefill call */
+  float eps;            /* RMSNorm eps (1e-5) */
+  int32_t tied;         /* lm_head shares the embedding table */
+} mx_llm_config;
+
+/* ---- library / memory -------------------------------------------------------------- */
+const char* mx_version(void);
+int mx_host_alloc(size_t bytes, void** host_ptr, void** dev_ptr); /* pinned, device-mapped */
+int mx_host_free(void* host_ptr);
+
+/* ---- LLM decoder (replaces vLLM / llama.cpp decode) -------------------------------- */
+int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out);
+/* names: embed, norm, lm_head (untied), l{i}.{attn_norm,wq,wk,wv,wo,mlp_norm,wg,wu,wd} */
+int mx_llm_set_weight(mx_llm* ctx, const char* name, const void* dev_data, int64_t numel,
+                      int dtype);
+/* RoPE tables [n_pos][head_dim/2] fp32 (host memory), llama3-scaled frequencies. */
+int mx_llm_set_rope(mx_llm* ctx, const float* cos_host, const float* sin_host, int n_pos);
+int mx_llm_finalize(mx_llm* ctx);
+/* Prefill prompt ids (host) into `slot`, bind the slot to decode row `row`, pick the first
+ * token greedily under `penalty` (engine_class.py:106-112).  Enqueued on `stream`. */
+int mx_llm_prefill(mx_llm* ctx, int slot, int row, const int32_t* ids_host, int n_ids,
+                   float penalty, void* stream);
+/* One greedy decode step for rows [0, n_rows) (hipGraph-captured per n_rows; replayed). */
+int mx_llm_decode(mx_llm* ctx, int n_rows, float penalty, void* stream);
+/* Same step launched eagerly with HIP events around each gate/up GEMV; adds the kernels'
+ * elapsed milliseconds to *gate_up_ms and their count to *n_launches (synchronises). */
+int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, float penalty, void* stream,
+                           double* gate_up_ms, int* n_launches);
+/* Park decode row `row` on the scratch slot (stream ended / barge-in reset). */
+int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
+/* Host-mapped token history [max_slots][max_pos] int32 written by the device. */
+int32_t* mx_llm_history(mx_llm* ctx);
+/* Parity/debug: keep a copy of the penalised logits of each decode row (enable before the
+ * first mx_llm_decode; costs one extra write per vocab entry) and read one row back. */
+int mx_llm_debug_logits(mx_llm* ctx, int enable);
+int mx_llm_read_logits(mx_llm* ctx, int row, float* host_out, void* stream);
+const char* mx_llm_last_error(const mx_llm* ctx);
+void mx_llm_destroy(mx_llm* ctx);
+
+/* ---- SNAC 24 kHz decoder (replaces SNAC.decode + slice + int16) --------------------- */
+int mx_snac_create(int device, int max_frames, int max_batch, mx_snac** out);
+/* names: q{i}.codebook [4096*8], q{i}.out_proj.w [768*8], q{i}.out_proj.b, in.dw.w [768*7],
+ * in.dw.b, in.pw.w [1024*768], in.pw.b, b{k}.alpha, b{k}.up.w [Cin*Cout*2s], b{k}.up.b,
+ * b{k}.noise.w, b{k}.r{j}.{alpha1,dw.w,dw.b,alpha2,pw.w,pw.b}, out.alpha, out.conv.w, out.conv.b
+ * (weight norm already folded; layouts as torch Conv1d / ConvTranspose1d weights). */
+int mx_snac_set_weight(mx_snac* ctx, const char* name, const void* dev_data, int64_t numel,
+                       int dtype);
+int mx_snac_finalize(mx_snac* ctx);
+/* Decode `batch` windows of n_frames frames each.  frames: [batch][7*n_frames] SNAC codes in
+ * speechpipe token order (0..4095; the caller applies the range check of speechpipe.py:108-111).
+ * noise: [batch][sum of the 4 NoiseBlock lengths] or NULL (fresh N(0,1) from `seed`).
+ * pcm: [batch][hi-lo] int16 of samples [lo,hi) (NULL to skip); audio: [batch][2048*n_frames]
+ * fp32 full window (NULL to skip). */
+int mx_snac_decode(mx_snac* ctx, const int32_t* frames, int n_frames, int batch,
+                   const float* noise, uint64_t seed, int16_t* pcm, float* audio, int lo,
+                   int hi, void* stream);
+const char* mx_snac_last_error(const mx_snac* ctx);
+void mx_snac_destroy(mx_snac* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MORPHEUS_MX_H */

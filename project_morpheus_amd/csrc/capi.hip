@@ -1,0 +1,798 @@
+// C ABI of libmorpheus_mx.so (include/morpheus_mx.h): context lifetime, weight packing,
+// the decode-step schedule, hipGraph capture/replay, and the SNAC window pipeline.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/morpheus_mx.h"
+#include "mx_llm_kernels.h"
+#include "mx_snac_kernels.h"
+
+using namespace mx;
+
+#define MX_TRY(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      (ctx)->err = std::string(#expr) + " -> " + hipGetErrorString(e_);               \
+      return MX_ERR_HIP;                                                               \
+    }                                                                                  \
+  } while (0)
+
+#define MX_FAIL(ctx, code, msg) \
+  do {                          \
+    (ctx)->err = (msg);         \
+    return (code);              \
+  } while (0)
+
+static thread_local std::string g_err;
+
+extern "C" const char* mx_version(void) { return "morpheus_mx 0.1 gfx950"; }
+
+extern "C" int mx_host_alloc(size_t bytes, void** host_ptr, void** dev_ptr) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+    return MX_ERR_OOM;
+  std::memset(h, 0, bytes);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return MX_ERR_HIP;
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return MX_OK;
+}
+
+extern "C" int mx_host_free(void* host_ptr) {
+  return hipHostFree(host_ptr) == hipSuccess ? MX_OK : MX_ERR_HIP;
+}
+
+// =====================================================================================
+// LLM context
+// =====================================================================================
+struct LayerW {
+  float* attn_norm = nullptr;
+  float* mlp_norm = nullptr;
+  uint16_t* wqkv = nullptr;  // [(H + 2*kvh*128)][H], q/k rows pair-interleaved for RoPE
+  uint16_t* wo = nullptr;    // [H][heads*128]
+  uint16_t* wgu = nullptr;   // [2F][H], rows (gate_i, up_i) interleaved
+  uint16_t* wd = nullptr;    // [H][F]
+  unsigned loaded = 0;
+};
+
+struct mx_llm {
+  int device = 0;
+  mx_llm_config c{};
+  std::string err;
+  std::vector<void*> allocs;
+  uint16_t* embed = nullptr;
+  uint16_t* lm = nullptr;
+  float* norm = nullptr;
+  std::vector<LayerW> L;
+  float* rope_cos = nullptr;
+  float* rope_sin = nullptr;
+  int rope_rows = 0;
+  uint16_t* kcache = nullptr;  // [layers][slots+1][kvh][max_pos][128]
+  uint16_t* vcache = nullptr;
+  size_t kv_layer_elems = 0;
+  float *h_dec = nullptr, *h_pre = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
+  float *part_ml = nullptr, *part_acc = nullptr;
+  int nsplit_max = 0;
+  int32_t *row_slot = nullptr, *row_pos = nullptr, *row_token = nullptr;
+  int32_t *pre_slot = nullptr, *pre_pos = nullptr, *pre_ids = nullptr;
+  unsigned long long* best = nullptr;
+  uint8_t* seen = nullptr;
+  float* penalty = nullptr;
+  float penalty_host = -1.f;
+  int32_t* hist_host = nullptr;
+  int32_t* hist_dev = nullptr;
+  hipStream_t cap = nullptr;
+  std::map<int, hipGraphExec_t> graphs;
+  std::map<int, hipGraph_t> graph_defs;
+  bool final = false;
+  int max_rows = 0;
+  float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
+
+  template <class T>
+  hipError_t alloc(T** p, size_t n) {
+    void* v = nullptr;
+    hipError_t e = hipMalloc(&v, n * sizeof(T) + 256);
+    if (e == hipSuccess) {
+      allocs.push_back(v);
+      *p = reinterpret_cast<T*>(v);
+    }
+    return e;
+  }
+};
+
+extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out) {
+  if (!cfg || !out) return MX_ERR_ARG;
+  auto* x = new mx_llm();
+  x->device = device;
+  x->c = *cfg;
+  const auto& c = x->c;
+  auto bad = [&](const char* m) {
+    g_err = m;
+    delete x;
+    return MX_ERR_ARG;
+  };
+  if (c.head_dim != 128) return bad("head_dim must be 128");
+  if (c.hidden % 256 || c.ffn % 256) return bad("hidden and ffn must be multiples of 256");
+  if (c.heads % c.kv_heads || c.heads / c.kv_heads > ATT_MAXG) return bad("bad GQA grouping");
+  if (c.heads * 128 % 256) return bad("heads*128 must be a multiple of 256");
+  if (c.max_pos % ATT_CHUNK) return bad("max_pos must be a multiple of 64");
+  if (c.max_batch < 1 || c.max_prefill < 1 || c.max_slots < 1) return bad("bad limits");
+  if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed");
+  x->L.resize(c.layers);
+  x->max_rows = c.max_batch > c.max_prefill ? c.max_batch : c.max_prefill;
+  x->nsplit_max = c.max_pos / ATT_CHUNK;
+  const int qkv_rows = c.heads * 128 + 2 * c.kv_heads * 128;
+  const int slots = c.max_slots + 1;  // +1 scratch slot for parked rows
+  x->kv_layer_elems = (size_t)slots * c.kv_heads * c.max_pos * 128;
+  hipError_t e = hipSuccess;
+#define A(p, n) \
+  if (e == hipSuccess) e = x->alloc(&(p), (size_t)(n));
+  A(x->embed, (size_t)c.vocab * c.hidden);
+  if (!c.tied) A(x->lm, (size_t)c.vocab * c.hidden);
+  A(x->norm, c.hidden);
+  for (auto& l : x->L) {
+    A(l.attn_norm, c.hidden);
+    A(l.mlp_norm, c.hidden);
+    A(l.wqkv, (size_t)qkv_rows * c.hidden);
+    A(l.wo, (size_t)c.hidden * c.heads * 128);
+    A(l.wgu, (size_t)2 * c.ffn * c.hidden);
+    A(l.wd, (size_t)c.hidden * c.ffn);
+  }
+  A(x->kcache, x->kv_layer_elems * c.layers);
+  A(x->vcache, x->kv_layer_elems * c.layers);
+  A(x->h_dec, (size_t)c.max_batch * c.hidden);
+  A(x->h_pre, (size_t)c.max_prefill * c.hidden);
+  A(x->q, (size_t)x->max_rows * c.heads * 128);
+  A(x->att, (size_t)x->max_rows * c.heads * 128);
+  A(x->act, (size_t)x->max_rows * c.ffn);
+  A(x->part_ml, (size_t)x->max_rows * c.heads * x->nsplit_max * 2);
+  A(x->part_acc, (size_t)x->max_rows * c.heads * x->nsplit_max * 128);
+  A(x->row_slot, c.max_batch);
+  A(x->row_pos, c.max_batch);
+  A(x->row_token, c.max_batch);
+  A(x->pre_slot, c.max_prefill);
+  A(x->pre_pos, c.max_prefill);
+  A(x->pre_ids, c.max_prefill);
+  A(x->best, c.max_batch);
+  A(x->seen, (size_t)slots * c.vocab);
+  A(x->penalty, 1);
+#undef A
+  if (c.tied) x->lm = x->embed;
+  if (e != hipSuccess) {
+    g_err = std::string("allocation failed: ") + hipGetErrorString(e);
+    for (void* p : x->allocs) (void)hipFree(p);
+    delete x;
+    return MX_ERR_OOM;
+  }
+  void* hh = nullptr;
+  void* hd = nullptr;
+  if (mx_host_alloc((size_t)slots * c.max_pos * sizeof(int32_t), &hh, &hd) != MX_OK) {
+    g_err = "host history alloc failed";
+    for (void* p : x->allocs) (void)hipFree(p);
+    delete x;
+    return MX_ERR_OOM;
+  }
+  x->hist_host = (int32_t*)hh;
+  x->hist_dev = (int32_t*)hd;
+  e = hipMemset(x->kcache, 0, x->kv_layer_elems * c.layers * 2);
+  if (e == hipSuccess) e = hipMemset(x->vcache, 0, x->kv_layer_elems * c.layers * 2);
+  if (e == hipSuccess) e = hipMemset(x->best, 0, c.max_batch * 8);
+  if (e == hipSuccess) e = hipMemset(x->seen, 0, (size_t)slots * c.vocab);
+  if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
+  // every decode row starts parked on the scratch slot at position 0
+  std::vector<int32_t> park(c.max_batch, c.max_slots), zero(c.max_batch, 0);
+  if (e == hipSuccess)
+    e = hipMemcpy(x->row_slot, park.data(), c.max_batch * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
+  if (e == hipSuccess) e = gemv_prepare();
+  if (e != hipSuccess) {
+    g_err = std::string("init failed: ") + hipGetErrorString(e);
+    mx_llm_destroy(x);
+    return MX_ERR_HIP;
+  }
+  *out = x;
+  return MX_OK;
+}
+
+// q/k rows of each head are reordered so that packed rows (2i, 2i+1) hold the RoPE
+// partners (i, i+64); v rows keep their order.  gate/up rows are interleaved (g_i, u_i).
+static int pack_rows(mx_llm* x, uint16_t* dst, const void* src, const std::vector<int32_t>& perm,
+                     int cols, int dtype) {
+  int32_t* dperm = nullptr;
+  MX_TRY(x, hipMalloc(&dperm, perm.size() * 4));
+  MX_TRY(x, hipMemcpy(dperm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice));
+  hipError_t e = launch_pack_rows(dst, src, dperm, (int)perm.size(), cols,
+                                  dtype == MX_DTYPE_F32 ? 1 : 0, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  (void)hipFree(dperm);
+  MX_TRY(x, e);
+  return MX_OK;
+}
+
+static int copy_f32(mx_llm* x, float* dst, const void* src, int64_t n, int dtype) {
+  MX_TRY(x, launch_to_f32(dst, src, n, dtype == MX_DTYPE_BF16 ? 1 : 0, nullptr));
+  MX_TRY(x, hipDeviceSynchronize());
+  return MX_OK;
+}
+
+extern "C" int mx_llm_set_weight(mx_llm* x, const char* name, const void* data, int64_t numel,
+                                 int dtype) {
+  if (!x || !name || !data) return MX_ERR_ARG;
+  if (dtype != MX_DTYPE_F32 && dtype != MX_DTYPE_BF16) MX_FAIL(x, MX_ERR_ARG, "bad dtype");
+  MX_TRY(x, hipSetDevice(x->device));
+  const auto& c = x->c;
+  const int H = c.hidden, F = c.ffn, QD = c.heads * 128, KD = c.kv_heads * 128;
+  const std::string n(name);
+  auto need = [&](int64_t want) { return numel == want; };
+  auto ident = [](int rows) {
+    std::vector<int32_t> p(rows);
+    for (int i = 0; i < rows; ++i) p[i] = i;
+    return p;
+  };
+  if (n == "embed" || n == "lm_head") {
+    if (!need((int64_t)c.vocab * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    if (n == "lm_head" && c.tied) MX_FAIL(x, MX_ERR_ARG, "lm_head given but config is tied");
+    return pack_rows(x, n == "embed" ? x->embed : x->lm, data, ident(c.vocab), H, dtype);
+  }
+  if (n == "norm") {
+    if (!need(H)) MX_FAIL(x, MX_ERR_ARG, "norm: bad numel");
+    return copy_f32(x, x->norm, data, H, dtype);
+  }
+  int li = -1;
+  char field[32] = {0};
+  if (std::sscanf(name, "l%d.%31s", &li, field) != 2 || li < 0 || li >= c.layers)
+    MX_FAIL(x, MX_ERR_ARG, "unknown weight " + n);
+  LayerW& l = x->L[li];
+  const std::string f(field);
+  // q/k/v are staged into one packed [qkv_rows][H] matrix at row offsets 0 / QD / QD+KD
+  auto qk_perm = [&](int heads) {
+    std::vector<int32_t> p(heads * 128);
+    for (int h = 0; h < heads; ++h)
+      for (int i = 0; i < 64; ++i) {
+        p[h * 128 + 2 * i] = h * 128 + i;
+        p[h * 128 + 2 * i + 1] = h * 128 + i + 64;
+      }
+    return p;
+  };
+  int rc = MX_OK;
+  if (f == "attn_norm" || f == "mlp_norm") {
+    if (!need(H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = copy_f32(x, f == "attn_norm" ? l.attn_norm : l.mlp_norm, data, H, dtype);
+    l.loaded |= f == "attn_norm" ? 1u : 2u;
+  } else if (f == "wq") {
+    if (!need((int64_t)QD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = pack_rows(x, l.wqkv, data, qk_perm(c.heads), H, dtype);
+    l.loaded |= 4u;
+  } else if (f == "wk") {
+    if (!need((int64_t)KD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = pack_rows(x, l.wqkv + (size_t)QD * H, data, qk_perm(c.kv_heads), H, dtype);
+    l.loaded |= 8u;
+  } else if (f == "wv") {
+    if (!need((int64_t)KD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = pack_rows(x, l.wqkv + (size_t)(QD + KD) * H, data, ident(KD), H, dtype);
+    l.loaded |= 16u;
+  } else if (f == "wo") {
+    if (!need((int64_t)H * QD)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = pack_rows(x, l.wo, data, ident(H), QD, dtype);
+    l.loaded |= 32u;
+  } else if (f == "wg" || f == "wu") {
+    if (!need((int64_t)F * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    // gate row i -> packed row 2i, up row i -> packed row 2i+1: pack into a temporary
+    // [F][H] then scatter with a strided view (two passes of the row-copy kernel)
+    std::vector<int32_t> p(F);
+    for (int i = 0; i < F; ++i) p[i] = i;
+    uint16_t* tmp = nullptr;
+    MX_TRY(x, hipMalloc(&tmp, (size_t)F * H * 2));
+    rc = pack_rows(x, tmp, data, p, H, dtype);
+    if (rc == MX_OK) {
+      const int off = f == "wg" ? 0 : 1;
+      hipError_t e = hipMemcpy2D(l.wgu + (size_t)off * H, (size_t)2 * H * 2, tmp, (size_t)H * 2,
+                                 (size_t)H * 2, F, hipMemcpyDeviceToDevice);
+      (void)hipFree(tmp);
+      MX_TRY(x, e);
+    } else {
+      (void)hipFree(tmp);
+    }
+    l.loaded |= f == "wg" ? 64u : 128u;
+  } else if (f == "wd") {
+    if (!need((int64_t)H * F)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    rc = pack_rows(x, l.wd, data, ident(H), F, dtype);
+    l.loaded |= 256u;
+  } else {
+    MX_FAIL(x, MX_ERR_ARG, "unknown weight " + n);
+  }
+  return rc;
+}
+
+extern "C" int mx_llm_set_rope(mx_llm* x, const float* cos_h, const float* sin_h, int n_pos) {
+  if (!x || !cos_h || !sin_h || n_pos < x->c.max_pos) {
+    if (x) x->err = "rope table must cover max_pos positions";
+    return MX_ERR_ARG;
+  }
+  MX_TRY(x, hipSetDevice(x->device));
+  const size_t n = (size_t)x->c.max_pos * 64;
+  if (!x->rope_cos) {
+    MX_TRY(x, x->alloc(&x->rope_cos, n));
+    MX_TRY(x, x->alloc(&x->rope_sin, n));
+  }
+  MX_TRY(x, hipMemcpy(x->rope_cos, cos_h, n * 4, hipMemcpyHostToDevice));
+  MX_TRY(x, hipMemcpy(x->rope_sin, sin_h, n * 4, hipMemcpyHostToDevice));
+  x->rope_rows = x->c.max_pos;
+  return MX_OK;
+}
+
+extern "C" int mx_llm_finalize(mx_llm* x) {
+  if (!x) return MX_ERR_ARG;
+  for (int i = 0; i < x->c.layers; ++i)
+    if (x->L[i].loaded != 511u)
+      MX_FAIL(x, MX_ERR_STATE, "layer " + std::to_string(i) + " weights incomplete");
+  if (!x->rope_cos) MX_FAIL(x, MX_ERR_STATE, "rope table not set");
+  x->final = true;
+  return MX_OK;
+}
+
+// ---- one forward over `R` rows (decode rows or prefill rows) -------------------------
+struct RowSet {
+  float* h;
+  const int32_t* slot;
+  const int32_t* pos;
+  int R;
+};
+
+static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st,
+                                 std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+  const auto& c = x->c;
+  const int H = c.hidden, QD = c.heads * 128;
+  const int qkv_rows = QD + 2 * c.kv_heads * 128;
+  hipError_t e = hipSuccess;
+  for (int li = 0; li < c.layers && e == hipSuccess; ++li) {
+    const LayerW& l = x->L[li];
+    uint16_t* kc = x->kcache + x->kv_layer_elems * li;
+    uint16_t* vc = x->vcache + x->kv_layer_elems * li;
+    GemvArgs g{};
+    g.R = rs.R;
+    g.eps = c.eps;
+    // QKV + RoPE + KV append
+    g.W = l.wqkv; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
+    g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
+    g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
+    g.max_pos = c.max_pos; g.Q = x->q;
+    e = launch_gemv(g, EPI_QKV, true, st);
+    if (e != hipSuccess) break;
+    AttnArgs at{};
+    at.Q = x->q; at.kcache = kc; at.vcache = vc; at.row_slot = rs.slot; at.row_pos = rs.pos;
+    at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
+    at.nsplit_max = x->nsplit_max; at.scale = 1.0f / sqrtf(128.0f);
+    at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.out = x->att;
+    e = launch_attention(at, rs.R, st);
+    if (e != hipSuccess) break;
+    // O projection + residual
+    GemvArgs o{};
+    o.R = rs.R; o.W = l.wo; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
+    o.ystride = H;
+    e = launch_gemv(o, EPI_RESID, false, st);
+    if (e != hipSuccess) break;
+    // gate/up + SiLU*up
+    GemvArgs gu{};
+    gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
+    gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act;
+    if (prof) {
+      prof->emplace_back();
+      (void)hipEventCreate(&prof->back().first);
+      (void)hipEventCreate(&prof->back().second);
+      (void)hipEventRecord(prof->back().first, st);
+    }
+    e = launch_gemv(gu, EPI_SILU, true, st);
+    if (prof) (void)hipEventRecord(prof->back().second, st);
+    if (e != hipSuccess) break;
+    // down + residual
+    GemvArgs d{};
+    d.R = rs.R; d.W = l.wd; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
+    d.ystride = H;
+    e = launch_gemv(d, EPI_RESID, false, st);
+  }
+  return e;
+}
+
+static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot, int R,
+                               unsigned long long* best, hipStream_t st) {
+  const auto& c = x->c;
+  GemvArgs g{};
+  g.R = R; g.eps = c.eps; g.W = x->lm; g.N = c.vocab; g.K = c.hidden; g.X = h;
+  g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
+  g.penalty = x->penalty; g.best = best;
+  g.logits = x->logits_dbg ? x->logits_dbg + (size_t)(best - x->best) * c.vocab : nullptr;
+  return launch_gemv(g, EPI_ARGMAX, true, st);
+}
+
+static hipError_t enqueue_decode(mx_llm* x, int n_rows, hipStream_t st,
+                                 std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+  const auto& c = x->c;
+  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows};
+  hipError_t e = enqueue_layers(x, rs, st, prof);
+  if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, n_rows, x->best, st);
+  if (e == hipSuccess) {
+    CommitArgs cm{};
+    cm.best = x->best; cm.row_slot = x->row_slot; cm.row_pos = x->row_pos;
+    cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
+    cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
+    cm.pos_advance = 1;
+    e = launch_commit(cm, n_rows, st);
+  }
+  return e;
+}
+
+static int set_penalty(mx_llm* x, float p, hipStream_t st) {
+  if (p != x->penalty_host) {
+    MX_TRY(x, launch_set_scalar(x->penalty, p, st));
+    x->penalty_host = p;
+  }
+  return MX_OK;
+}
+
+extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, int n,
+                              float penalty, void* stream) {
+  if (!x || !ids) return MX_ERR_ARG;
+  if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
+  const auto& c = x->c;
+  if (slot < 0 || slot >= c.max_slots || row < 0 || row >= c.max_batch)
+    MX_FAIL(x, MX_ERR_ARG, "slot/row out of range");
+  if (n < 1 || n > c.max_prefill || n >= c.max_pos) MX_FAIL(x, MX_ERR_ARG, "bad prompt length");
+  for (int i = 0; i < n; ++i)
+    if (ids[i] < 0 || ids[i] >= c.vocab) MX_FAIL(x, MX_ERR_ARG, "prompt id out of vocab");
+  hipStream_t st = (hipStream_t)stream;
+  MX_TRY(x, hipSetDevice(x->device));
+  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
+  MX_TRY(x, hipMemsetAsync(x->seen + (size_t)slot * c.vocab, 0, c.vocab, st));
+  MX_TRY(x, hipMemcpyAsync(x->pre_ids, ids, (size_t)n * 4, hipMemcpyHostToDevice, st));
+  MX_TRY(x, launch_set_rows(x->pre_slot, x->pre_pos, n, slot, 0, st));
+  MX_TRY(x, launch_embed_rows(x->pre_ids, n, slot, x->embed, c.hidden, c.vocab, x->seen,
+                              x->h_pre, st));
+  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n};
+  MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
+  MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
+  MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1), 1,
+                         x->best + row, st));
+  // bind decode row -> slot at position n-1, then commit (advances to n)
+  MX_TRY(x, launch_set_rows(x->row_slot + row, x->row_pos + row, 1, slot, n - 1, st));
+  CommitArgs cm{};
+  cm.best = x->best + row; cm.row_slot = x->row_slot + row; cm.row_pos = x->row_pos + row;
+  cm.row_token = x->row_token + row; cm.seen = x->seen; cm.hist = x->hist_dev;
+  cm.embed = x->embed; cm.h = x->h_dec + (size_t)row * c.hidden; cm.hidden = c.hidden;
+  cm.vocab = c.vocab; cm.max_pos = c.max_pos; cm.pos_advance = 1;
+  MX_TRY(x, launch_commit(cm, 1, st));
+  return MX_OK;
+}
+
+extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream) {
+  if (!x) return MX_ERR_ARG;
+  if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
+  if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
+  hipStream_t st = (hipStream_t)stream;
+  MX_TRY(x, hipSetDevice(x->device));
+  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
+  auto it = x->graphs.find(n_rows);
+  if (it == x->graphs.end()) {
+    // capture on the private stream; kernels read row positions from device memory so
+    // one graph serves every step
+    MX_TRY(x, hipStreamSynchronize(st));
+    MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
+    hipError_t e = enqueue_decode(x, n_rows, x->cap, nullptr);
+    hipGraph_t g = nullptr;
+    hipError_t e2 = hipStreamEndCapture(x->cap, &g);
+    MX_TRY(x, e);
+    MX_TRY(x, e2);
+    hipGraphExec_t ex = nullptr;
+    MX_TRY(x, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    x->graph_defs[n_rows] = g;
+    it = x->graphs.emplace(n_rows, ex).first;
+  }
+  MX_TRY(x, hipGraphLaunch(it->second, st));
+  return MX_OK;
+}
+
+extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, float penalty, void* stream,
+                                      double* gate_up_ms, int* n_launches) {
+  if (!x) return MX_ERR_ARG;
+  if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
+  if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
+  hipStream_t st = (hipStream_t)stream;
+  MX_TRY(x, hipSetDevice(x->device));
+  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  hipError_t e = enqueue_decode(x, n_rows, st, &ev);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  double tot = 0.0;
+  for (auto& p : ev) {
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, p.first, p.second);
+    tot += ms;
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  MX_TRY(x, e);
+  if (gate_up_ms) *gate_up_ms += tot;
+  if (n_launches) *n_launches += (int)ev.size();
+  return MX_OK;
+}
+
+extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
+  if (!x || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, launch_set_rows(x->row_slot + row, x->row_pos + row, 1, x->c.max_slots, 0,
+                            (hipStream_t)stream));
+  return MX_OK;
+}
+
+extern "C" int32_t* mx_llm_history(mx_llm* x) { return x ? x->hist_host : nullptr; }
+
+extern "C" int mx_llm_debug_logits(mx_llm* x, int enable) {
+  if (!x) return MX_ERR_ARG;
+  if (!x->graphs.empty()) MX_FAIL(x, MX_ERR_STATE, "enable logits before the first decode");
+  MX_TRY(x, hipSetDevice(x->device));
+  if (enable && !x->logits_dbg) MX_TRY(x, x->alloc(&x->logits_dbg, (size_t)x->c.max_batch * x->c.vocab));
+  if (!enable) x->logits_dbg = nullptr;
+  return MX_OK;
+}
+
+extern "C" int mx_llm_read_logits(mx_llm* x, int row, float* host_out, void* stream) {
+  if (!x || !host_out || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
+  if (!x->logits_dbg) MX_FAIL(x, MX_ERR_STATE, "logits not enabled");
+  MX_TRY(x, hipMemcpyAsync(host_out, x->logits_dbg + (size_t)row * x->c.vocab,
+                           (size_t)x->c.vocab * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  MX_TRY(x, hipStreamSynchronize((hipStream_t)stream));
+  return MX_OK;
+}
+
+extern "C" const char* mx_llm_last_error(const mx_llm* x) {
+  return x ? x->err.c_str() : g_err.c_str();
+}
+
+extern "C" void mx_llm_destroy(mx_llm* x) {
+  if (!x) return;
+  (void)hipSetDevice(x->device);
+  for (auto& kv : x->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : x->graph_defs) (void)hipGraphDestroy(kv.second);
+  if (x->cap) (void)hipStreamDestroy(x->cap);
+  for (void* p : x->allocs) (void)hipFree(p);
+  if (x->hist_host) (void)hipHostFree(x->hist_host);
+  delete x;
+}
+
+// =====================================================================================
+// SNAC context
+// =====================================================================================
+static const int kRates[4] = {8, 8, 4, 2};
+static const int kDil[3] = {1, 3, 9};
+
+struct mx_snac {
+  int device = 0;
+  int max_frames = 0, max_batch = 0;
+  std::string err;
+  std::map<std::string, float*> w;
+  std::map<std::string, int64_t> expect;
+  std::vector<void*> allocs;
+  float* up_packed[4][8] = {};  // per block, per phase: [Cout][2*Cin]
+  int up_delta[4][8][2] = {};
+  float *bufA = nullptr, *bufB = nullptr, *noise = nullptr;
+  size_t buf_elems = 0;
+  bool final = false;
+};
+
+static void snac_expect(mx_snac* s) {
+  auto& e = s->expect;
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = "q" + std::to_string(i) + ".";
+    e[p + "codebook"] = 4096 * 8;
+    e[p + "out_proj.w"] = 768 * 8;
+    e[p + "out_proj.b"] = 768;
+  }
+  e["in.dw.w"] = 768 * 7;
+  e["in.dw.b"] = 768;
+  e["in.pw.w"] = 1024 * 768;
+  e["in.pw.b"] = 1024;
+  for (int b = 0; b < 4; ++b) {
+    const int cin = 1024 >> b, cout = cin / 2, s = kRates[b];
+    const std::string p = "b" + std::to_string(b) + ".";
+    e[p + "alpha"] = cin;
+    e[p + "up.w"] = (int64_t)cin * cout * 2 * s;
+    e[p + "up.b"] = cout;
+    e[p + "noise.w"] = (int64_t)cout * cout;
+    for (int r = 0; r < 3; ++r) {
+      const std::string q = p + "r" + std::to_string(r) + ".";
+      e[q + "alpha1"] = cout;
+      e[q + "dw.w"] = cout * 7;
+      e[q + "dw.b"] = cout;
+      e[q + "alpha2"] = cout;
+      e[q + "pw.w"] = (int64_t)cout * cout;
+      e[q + "pw.b"] = cout;
+    }
+  }
+  e["out.alpha"] = 64;
+  e["out.conv.w"] = 64 * 7;
+  e["out.conv.b"] = 1;
+}
+
+extern "C" int mx_snac_create(int device, int max_frames, int max_batch, mx_snac** out) {
+  if (!out || max_frames < 1 || max_batch < 1) return MX_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) {
+    g_err = "hipSetDevice failed";
+    return MX_ERR_HIP;
+  }
+  auto* s = new mx_snac();
+  s->device = device;
+  s->max_frames = max_frames;
+  s->max_batch = max_batch;
+  snac_expect(s);
+  s->buf_elems = (size_t)131072 * max_frames * max_batch;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, s->buf_elems * 4);
+  if (e == hipSuccess) { s->allocs.push_back(p); s->bufA = (float*)p; e = hipMalloc(&p, s->buf_elems * 4); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->bufB = (float*)p; e = hipMalloc(&p, (size_t)3360 * max_frames * max_batch * 4); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->noise = (float*)p; }
+  if (e != hipSuccess) {
+    g_err = std::string("snac alloc failed: ") + hipGetErrorString(e);
+    for (void* q : s->allocs) (void)hipFree(q);
+    delete s;
+    return MX_ERR_OOM;
+  }
+  *out = s;
+  return MX_OK;
+}
+
+extern "C" int mx_snac_set_weight(mx_snac* s, const char* name, const void* data, int64_t numel,
+                                  int dtype) {
+  if (!s || !name || !data) return MX_ERR_ARG;
+  const std::string n(name);
+  auto it = s->expect.find(n);
+  if (it == s->expect.end()) MX_FAIL(s, MX_ERR_ARG, "unknown snac weight " + n);
+  if (it->second != numel) MX_FAIL(s, MX_ERR_ARG, n + ": bad numel");
+  MX_TRY(s, hipSetDevice(s->device));
+  float* d = nullptr;
+  auto f = s->w.find(n);
+  if (f == s->w.end()) {
+    void* p = nullptr;
+    MX_TRY(s, hipMalloc(&p, numel * 4 + 256));
+    s->allocs.push_back(p);
+    d = (float*)p;
+    s->w[n] = d;
+  } else {
+    d = f->second;
+  }
+  MX_TRY(s, launch_to_f32(d, data, numel, dtype == MX_DTYPE_BF16 ? 1 : 0, nullptr));
+  MX_TRY(s, hipDeviceSynchronize());
+  return MX_OK;
+}
+
+extern "C" int mx_snac_finalize(mx_snac* s) {
+  if (!s) return MX_ERR_ARG;
+  for (auto& kv : s->expect)
+    if (!s->w.count(kv.first)) MX_FAIL(s, MX_ERR_STATE, "missing snac weight " + kv.first);
+  MX_TRY(s, hipSetDevice(s->device));
+  // ConvTranspose1d(k=2s, stride s, pad ceil(s/2)) as s phase GEMMs with 2 taps each:
+  // out[co][s*t+ph] = sum_ci W[ci][co][rm] x[ci][t+q] + W[ci][co][rm+s] x[ci][t+q-1],
+  // q = (ph+p) / s, rm = (ph+p) % s.
+  for (int b = 0; b < 4; ++b) {
+    const int cin = 1024 >> b, cout = cin / 2, st = kRates[b], k = 2 * st, pad = (st + 1) / 2;
+    const std::string name = "b" + std::to_string(b) + ".up.w";
+    std::vector<float> W((size_t)cin * cout * k);
+    MX_TRY(s, hipMemcpy(W.data(), s->w[name], W.size() * 4, hipMemcpyDeviceToHost));
+    for (int ph = 0; ph < st; ++ph) {
+      const int q = (ph + pad) / st, rm = (ph + pad) % st;
+      std::vector<float> A((size_t)cout * 2 * cin);
+      for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < cin; ++ci) {
+          A[(size_t)co * 2 * cin + ci] = W[((size_t)ci * cout + co) * k + rm];
+          A[(size_t)co * 2 * cin + cin + ci] = W[((size_t)ci * cout + co) * k + rm + st];
+        }
+      if (!s->up_packed[b][ph]) {
+        void* p = nullptr;
+        MX_TRY(s, hipMalloc(&p, A.size() * 4));
+        s->allocs.push_back(p);
+        s->up_packed[b][ph] = (float*)p;
+      }
+      MX_TRY(s, hipMemcpy(s->up_packed[b][ph], A.data(), A.size() * 4, hipMemcpyHostToDevice));
+      s->up_delta[b][ph][0] = q;
+      s->up_delta[b][ph][1] = q - 1;
+    }
+  }
+  s->final = true;
+  return MX_OK;
+}
+
+extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, int batch,
+                              const float* noise, uint64_t seed, int16_t* pcm, float* audio,
+                              int lo, int hi, void* stream) {
+  if (!s || !frames) return MX_ERR_ARG;
+  if (!s->final) MX_FAIL(s, MX_ERR_STATE, "not finalized");
+  if (n_frames < 1 || n_frames > s->max_frames || batch < 1 || batch > s->max_batch)
+    MX_FAIL(s, MX_ERR_ARG, "n_frames/batch out of range");
+  const int Tout = 2048 * n_frames;
+  if (pcm && (lo < 0 || hi < lo)) MX_FAIL(s, MX_ERR_ARG, "bad slice");
+  if (hi > Tout) hi = Tout;  // torch slicing clamps: [2048:4096] of a 2048-sample window is empty
+  if (lo > hi) lo = hi;
+  hipStream_t st = (hipStream_t)stream;
+  MX_TRY(s, hipSetDevice(s->device));
+  auto W = [&](const std::string& n) { return s->w[n]; };
+  const int B = batch;
+  int T = 4 * n_frames;
+  float* x = s->bufA;
+  float* y = s->bufB;
+  // noise layout per window: [32N | 256N | 1024N | 2048N]
+  const int nlen = 3360 * n_frames;
+  const float* nz = noise;
+  if (!nz) {
+    MX_TRY(s, launch_gauss(s->noise, (int64_t)nlen * B, seed, st));
+    nz = s->noise;
+  }
+  const float* cb[3] = {W("q0.codebook"), W("q1.codebook"), W("q2.codebook")};
+  const float* pw[3] = {W("q0.out_proj.w"), W("q1.out_proj.w"), W("q2.out_proj.w")};
+  const float* pb[3] = {W("q0.out_proj.b"), W("q1.out_proj.b"), W("q2.out_proj.b")};
+  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, x, st));        // x: [768][T]
+  MX_TRY(s, launch_dwconv(x, y, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
+  {
+    ConvGemmArgs g{};
+    g.A = W("in.pw.w"); g.X = y; g.bias = W("in.pw.b"); g.out = x; g.M = 1024; g.Cin = 768;
+    g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_STORE;
+    MX_TRY(s, launch_conv_gemm(g, B, st));                                      // x: [1024][T]
+  }
+  int noff = 0;
+  for (int b = 0; b < 4; ++b) {
+    const int cin = 1024 >> b, cout = cin / 2, sr = kRates[b];
+    const std::string p = "b" + std::to_string(b) + ".";
+    const int To = T * sr;
+    for (int ph = 0; ph < sr; ++ph) {  // Snake + ConvTranspose1d: x [cin][T] -> y [cout][To]
+      ConvGemmArgs g{};
+      g.A = s->up_packed[b][ph]; g.X = x; g.alpha = W(p + "alpha"); g.bias = W(p + "up.b");
+      g.out = y; g.M = cout; g.Cin = cin; g.Tin = T; g.Tout = To; g.nseg = 2;
+      g.delta[0] = s->up_delta[b][ph][0]; g.delta[1] = s->up_delta[b][ph][1];
+      g.col_stride = sr; g.col_off = ph; g.epi = CG_STORE;
+      MX_TRY(s, launch_conv_gemm(g, B, st));
+    }
+    T = To;
+    {  // NoiseBlock: x = y + noise * (Wn y)
+      ConvGemmArgs g{};
+      g.A = W(p + "noise.w"); g.X = y; g.R = y; g.noise = nz + noff; g.noise_stride = nlen;
+      g.out = x; g.M = cout;
+      g.Cin = cout; g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_NOISE;
+      MX_TRY(s, launch_conv_gemm(g, B, st));
+    }
+    noff += T;
+    for (int r = 0; r < 3; ++r) {  // ResidualUnit(d): x += pw(Snake(dw_d(Snake(x))))
+      const std::string q = p + "r" + std::to_string(r) + ".";
+      MX_TRY(s, launch_dwconv(x, y, W(q + "dw.w"), W(q + "dw.b"), W(q + "alpha1"),
+                              W(q + "alpha2"), B, cout, T, kDil[r], st));
+      ConvGemmArgs g{};
+      g.A = W(q + "pw.w"); g.X = y; g.bias = W(q + "pw.b"); g.R = x; g.out = x; g.M = cout;
+      g.Cin = cout; g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_RESID;
+      MX_TRY(s, launch_conv_gemm(g, B, st));
+    }
+  }
+  MX_TRY(s, launch_snac_out(x, W("out.alpha"), W("out.conv.w"), W("out.conv.b"), B, T, lo, hi,
+                            audio, pcm, st));
+  return MX_OK;
+}
+
+extern "C" const char* mx_snac_last_error(const mx_snac* s) {
+  return s ? s->err.c_str() : g_err.c_str();
+}
+
+extern "C" void mx_snac_destroy(mx_snac* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  for (void* p : s->allocs) (void)hipFree(p);
+  delete s;
+}

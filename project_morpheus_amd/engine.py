@@ -1,0 +1,314 @@
+"""Host side of the MI355X path: LLM and SNAC contexts, and the utterance runner.
+
+* ``LlmEngine``   wraps mx_llm_* (replaces vLLM ``AsyncLLMEngine.generate``,
+                  engine_class.py:117, and llama.cpp ``Llama``, llama_local.py:42-52).
+* ``SnacDecoder`` wraps mx_snac_* (replaces ``SNAC.decode`` + slice + PCM16,
+                  speechpipe.py:76-129).
+* ``Synthesizer`` is the Orpheus decoder loop (engine_class.py:103-134 +
+                  speechpipe.py:191-337) at the token-id level: prefill, hipGraph decode
+                  steps kept ``depth`` deep in the GPU queue, the reference's window schedule
+                  on the host, SNAC windows on a second HIP stream, PCM read from
+                  host-mapped memory.  No per-token string formatting, no per-token sync.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterator, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import STOP_IDS, OrpheusConfig, rope_tables
+from .schedule import WindowScheduler, code_of_id
+
+SAMPLES_PER_FRAME = 2048
+SLICE_LO, SLICE_HI = 2048, 4096
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return _lib.MX_DTYPE_BF16
+    if t.dtype == torch.float32:
+        return _lib.MX_DTYPE_F32
+    raise TypeError(f"unsupported weight dtype {t.dtype}")
+
+
+class LlmEngine:
+    """One mx_llm context on one GPU (weights replicated per GPU)."""
+
+    def __init__(self, cfg: OrpheusConfig, weights: Dict[str, torch.Tensor], device: int = 0,
+                 max_slots: int = 4, max_pos: int = 2048, max_batch: int = 1,
+                 max_prefill: int = 256):
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.cfg, self.device = cfg, device
+        self.max_slots, self.max_pos, self.max_batch = max_slots, max_pos, max_batch
+        self.max_prefill = max_prefill
+        c = _lib.LlmConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                           kv_heads=cfg.kv_heads, head_dim=cfg.head_dim, ffn=cfg.ffn,
+                           vocab=cfg.vocab, max_slots=max_slots, max_pos=max_pos,
+                           max_batch=max_batch, max_prefill=max_prefill, eps=cfg.eps,
+                           tied=int(cfg.tied))
+        h = C.c_void_p()
+        torch.cuda.set_device(device)
+        rc = self.lib.mx_llm_create(device, C.byref(c), C.byref(h))
+        _lib.check(rc, self.lib.mx_llm_last_error, None)
+        self.h = h
+        dev = torch.device("cuda", device)
+        for name, t in weights.items():
+            td = t.to(dev).contiguous()
+            rc = self.lib.mx_llm_set_weight(h, name.encode(), C.c_void_p(td.data_ptr()),
+                                            td.numel(), _dtype_code(td))
+            self._check(rc)
+            del td
+        cos, sin = rope_tables(cfg, max_pos)
+        self._check(self.lib.mx_llm_set_rope(h, cos.ctypes.data, sin.ctypes.data, max_pos))
+        self._check(self.lib.mx_llm_finalize(h))
+        hp = self.lib.mx_llm_history(h)
+        n = (max_slots + 1) * max_pos
+        self.hist = np.ctypeslib.as_array(hp, shape=(n,)).reshape(max_slots + 1, max_pos)
+        torch.cuda.synchronize(device)
+
+    def _check(self, rc):
+        _lib.check(rc, self.lib.mx_llm_last_error, self.h)
+
+    def prefill(self, slot: int, row: int, ids: Sequence[int], penalty: float, stream) -> None:
+        arr = np.ascontiguousarray(np.asarray(ids, dtype=np.int32))
+        self._check(self.lib.mx_llm_prefill(self.h, slot, row, arr.ctypes.data, len(arr),
+                                            penalty, C.c_void_p(stream.cuda_stream)))
+
+    def decode(self, n_rows: int, penalty: float, stream) -> None:
+        self._check(self.lib.mx_llm_decode(self.h, n_rows, penalty,
+                                           C.c_void_p(stream.cuda_stream)))
+
+    def decode_profiled(self, n_rows: int, penalty: float, stream):
+        ms, n = C.c_double(0.0), C.c_int(0)
+        self._check(self.lib.mx_llm_decode_profiled(self.h, n_rows, penalty,
+                                                    C.c_void_p(stream.cuda_stream),
+                                                    C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def enable_logits(self) -> None:
+        """Parity/debug mode: keep the penalised logits of each row (before first decode)."""
+        self._check(self.lib.mx_llm_debug_logits(self.h, 1))
+
+    def read_logits(self, row: int, stream) -> np.ndarray:
+        out = np.empty(self.cfg.vocab, dtype=np.float32)
+        self._check(self.lib.mx_llm_read_logits(self.h, row, out.ctypes.data,
+                                                C.c_void_p(stream.cuda_stream)))
+        return out
+
+    def release_row(self, row: int, stream) -> None:
+        self._check(self.lib.mx_llm_release_row(self.h, row, C.c_void_p(stream.cuda_stream)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mx_llm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SnacDecoder:
+    """One mx_snac context (fp32 SNAC 24 kHz decoder)."""
+
+    NOISE_PER_FRAME = 3360  # 32 + 256 + 1024 + 2048 samples of NoiseBlock noise per frame
+
+    def __init__(self, weights: Dict[str, torch.Tensor], device: int = 0, max_frames: int = 7,
+                 max_batch: int = 1):
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.device, self.max_frames, self.max_batch = device, max_frames, max_batch
+        h = C.c_void_p()
+        torch.cuda.set_device(device)
+        _lib.check(self.lib.mx_snac_create(device, max_frames, max_batch, C.byref(h)),
+                   self.lib.mx_snac_last_error, None)
+        self.h = h
+        dev = torch.device("cuda", device)
+        for name, t in weights.items():
+            td = t.to(dev).contiguous()
+            self._check(self.lib.mx_snac_set_weight(h, name.encode(), C.c_void_p(td.data_ptr()),
+                                                    td.numel(), _dtype_code(td)))
+        self._check(self.lib.mx_snac_finalize(h))
+        torch.cuda.synchronize(device)
+
+    def _check(self, rc):
+        _lib.check(rc, self.lib.mx_snac_last_error, self.h)
+
+    def decode_ptr(self, frames_ptr: int, n_frames: int, batch: int, noise_ptr: int, seed: int,
+                   pcm_ptr: int, audio_ptr: int, lo: int, hi: int, stream) -> None:
+        self._check(self.lib.mx_snac_decode(self.h, C.c_void_p(frames_ptr), n_frames, batch,
+                                            C.c_void_p(noise_ptr), seed, C.c_void_p(pcm_ptr),
+                                            C.c_void_p(audio_ptr), lo, hi,
+                                            C.c_void_p(stream.cuda_stream)))
+
+    def decode(self, codes: torch.Tensor, noise: Optional[torch.Tensor] = None, seed: int = 0,
+               lo: int = SLICE_LO, hi: int = SLICE_HI, want_audio: bool = False, stream=None):
+        """codes [B, 7N] int32 (device) -> (pcm int16 [B, hi'-lo'], audio fp32 [B, 2048N]|None)."""
+        stream = stream or torch.cuda.current_stream(self.device)
+        codes = codes.to(torch.int32).contiguous()
+        B, n7 = codes.shape
+        n = n7 // 7
+        hi_c = min(hi, SAMPLES_PER_FRAME * n)
+        lo_c = min(lo, hi_c)
+        pcm = torch.empty(B, hi_c - lo_c, dtype=torch.int16, device=codes.device)
+        audio = torch.empty(B, SAMPLES_PER_FRAME * n, dtype=torch.float32,
+                            device=codes.device) if want_audio else None
+        if noise is not None:
+            noise = noise.to(torch.float32).contiguous()
+            assert noise.shape == (B, self.NOISE_PER_FRAME * n)
+        self.decode_ptr(codes.data_ptr(), n, B, noise.data_ptr() if noise is not None else 0,
+                        seed, pcm.data_ptr() if pcm.numel() else 0,
+                        audio.data_ptr() if audio is not None else 0, lo_c, hi_c, stream)
+        return pcm, audio
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mx_snac_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class UtteranceStats:
+    tokens: int = 0
+    windows: int = 0
+    samples: int = 0
+    t_start: float = 0.0
+    t_first_audio: Optional[float] = None
+    t_end: float = 0.0
+    token_ids: List[int] = field(default_factory=list)
+
+    @property
+    def audio_seconds(self) -> float:
+        return self.samples / 24000.0
+
+    @property
+    def first_audio_ms(self) -> Optional[float]:
+        return None if self.t_first_audio is None else 1e3 * (self.t_first_audio - self.t_start)
+
+
+class _WindowRing:
+    """Host-mapped staging for SNAC windows: codes in, PCM16 out, zero-copy."""
+
+    def __init__(self, n: int = 32, max_frames: int = 7):
+        self.n = n
+        self.codes_bytes = 7 * max_frames * 4
+        self.buf = _lib.HostBuffer(n * (self.codes_bytes + 4096))
+        self.codes = [self.buf.view(np.int32, 7 * max_frames, i * self.codes_bytes)
+                      for i in range(n)]
+        base = n * self.codes_bytes
+        self.pcm = [self.buf.view(np.int16, 2048, base + i * 4096) for i in range(n)]
+        self.codes_dev = [self.buf.dev_ptr(i * self.codes_bytes) for i in range(n)]
+        self.pcm_dev = [self.buf.dev_ptr(base + i * 4096) for i in range(n)]
+
+
+class Synthesizer:
+    """The per-GPU decoder loop.  ``run`` yields PCM16 bytes chunks in order."""
+
+    def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: int = 3, seed: int = 0):
+        self.llm, self.snac = llm, snac
+        self.depth = depth
+        self.stream = torch.cuda.Stream(llm.device)
+        self.snac_stream = torch.cuda.Stream(llm.device)
+        self.ring = _WindowRing(32, snac.max_frames)
+        self.seed = seed
+        self._windows = 0
+
+    def run(self, prompt_ids: Sequence[int], max_tokens: int, penalty: float = 1.1,
+            stop_ids: Sequence[int] = STOP_IDS, inject_ids: Optional[Sequence[int]] = None,
+            stats: Optional[UtteranceStats] = None, slot: int = 0, row: int = 0,
+            noise_fn: Optional[Callable[[int], int]] = None) -> Iterator[bytes]:
+        """Prefill, then greedy-decode up to ``max_tokens`` tokens (engine_class.py:103-134).
+
+        ``inject_ids`` (bench / synthetic weights): token ids fed to the SNAC
+        schedule in place of the model's own tokens; the LLM still decodes every step.
+        """
+        st = stats if stats is not None else UtteranceStats()
+        st.t_start = time.perf_counter()
+        llm, n0 = self.llm, len(prompt_ids)
+        max_tokens = min(max_tokens, llm.max_pos - n0)
+        sched = WindowScheduler()
+        pending: deque = deque()   # (ring index, event, n_frames, nbytes)
+        inflight: deque = deque()  # (token index, event)
+        stop = set(int(s) for s in stop_ids)
+
+        llm.prefill(slot, row, prompt_ids, penalty, self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        inflight.append((0, ev))
+        launched, done, stopped = 1, 0, False
+
+        def launch_window(win: List[int]):
+            i = self._windows % self.ring.n
+            if len(pending) >= self.ring.n:
+                yield from drain(block=True, upto=1)
+            nf = len(win) // 7
+            self.ring.codes[i][: 7 * nf] = win[: 7 * nf]
+            lo, hi = SLICE_LO, min(SLICE_HI, SAMPLES_PER_FRAME * nf)
+            self.snac.decode_ptr(self.ring.codes_dev[i], nf, 1, 0,
+                                 (self.seed * 1000003 + self._windows) & 0xFFFFFFFFFFFF,
+                                 self.ring.pcm_dev[i], 0, lo, max(lo, hi), self.snac_stream)
+            e = torch.cuda.Event()
+            e.record(self.snac_stream)
+            pending.append((i, e, max(0, hi - lo) * 2))
+            self._windows += 1
+            st.windows += 1
+
+        def drain(block: bool, upto: Optional[int] = None):
+            k = 0
+            while pending and (upto is None or k < upto):
+                i, e, nbytes = pending[0]
+                if not block and not e.query():
+                    return
+                e.synchronize()
+                pending.popleft()
+                k += 1
+                if nbytes:
+                    data = self.ring.pcm[i][: nbytes // 2].tobytes()
+                    st.samples += nbytes // 2
+                    if st.t_first_audio is None:
+                        st.t_first_audio = time.perf_counter()
+                    yield data
+
+        while done < max_tokens:
+            while (not stopped and launched < max_tokens and launched - done < self.depth):
+                llm.decode(1, penalty, self.stream)
+                e = torch.cuda.Event()
+                e.record(self.stream)
+                inflight.append((launched, e))
+                launched += 1
+            k, e = inflight.popleft()
+            e.synchronize()
+            tok = int(llm.hist[slot, n0 + k])
+            done += 1
+            st.tokens += 1
+            st.token_ids.append(tok)
+            feed = int(inject_ids[k]) if inject_ids is not None else tok
+            for win in sched.push(code_of_id(feed, sched.count)):
+                yield from launch_window(win)
+            yield from drain(block=False)
+            if tok in stop:
+                stopped = True
+                break
+        # drain speculative steps still in flight (their tokens are discarded)
+        for _, e in inflight:
+            e.synchronize()
+        for win in sched.flush():
+            yield from launch_window(win)
+        yield from drain(block=True)
+        llm.release_row(row, self.stream)
+        st.t_end = time.perf_counter()

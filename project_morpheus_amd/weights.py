@@ -1,0 +1,192 @@
+"""Weight sources: seeded synthetic weights of the exact shapes, and local checkpoints.
+
+No checkpoint or network is available in this environment (SURVEY.md §7 "Hard parts"), so
+benchmarks and parity tests run on seeded synthetic weights (N(0, 0.02)
+matrices, unit norms, bf16).  Real weights load from local paths only:
+
+* Orpheus/Llama: a HF directory with ``config.json`` + ``*.safetensors``
+  (``model.layers.{i}.self_attn.q_proj.weight`` ... naming).
+* SNAC 24 kHz: a ``pytorch_model.bin`` / ``*.safetensors`` state dict of
+  ``snac.SNAC`` (``decoder.model.{i}...``), weight norm folded here:
+  w = g * v / ||v|| over every dim but 0 (torch weight_norm, dim=0).
+  The key mapping follows snac 1.2.x's module tree and is UNVERIFIED until a checkpoint
+  is supplied.
+"""
+from __future__ import annotations
+
+import glob
+import math
+import os
+from typing import Dict
+
+import torch
+
+from .config import OrpheusConfig
+
+LLM_LAYER_FIELDS = ("attn_norm", "wq", "wk", "wv", "wo", "mlp_norm", "wg", "wu", "wd")
+SNAC_RATES = (8, 8, 4, 2)
+
+
+def llm_shapes(cfg: OrpheusConfig) -> Dict[str, tuple]:
+    H, QD, KD, F = cfg.hidden, cfg.heads * cfg.head_dim, cfg.kv_heads * cfg.head_dim, cfg.ffn
+    s = {"embed": (cfg.vocab, H), "norm": (H,)}
+    if not cfg.tied:
+        s["lm_head"] = (cfg.vocab, H)
+    for i in range(cfg.layers):
+        p = f"l{i}."
+        s.update({p + "attn_norm": (H,), p + "wq": (QD, H), p + "wk": (KD, H),
+                  p + "wv": (KD, H), p + "wo": (H, QD), p + "mlp_norm": (H,),
+                  p + "wg": (F, H), p + "wu": (F, H), p + "wd": (H, F)})
+    return s
+
+
+def synthetic_llm_weights(cfg: OrpheusConfig, seed: int = 0, device="cpu",
+                          std: float = 0.02, norm_jitter: float = 0.0):
+    """N(0, std) bf16 matrices and (1 + jitter) norms, drawn in ``llm_shapes`` order."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = {}
+    for name, shape in llm_shapes(cfg).items():
+        if len(shape) == 1:
+            w = torch.ones(shape, device=device)
+            if norm_jitter:
+                w += norm_jitter * (torch.rand(shape, generator=g, device=device) - 0.5)
+            out[name] = w.to(torch.bfloat16)
+        else:
+            w = torch.empty(shape, device=device, dtype=torch.float32)
+            w.normal_(0.0, std, generator=g)
+            out[name] = w.to(torch.bfloat16)
+            del w
+    return out
+
+
+def load_hf_llm(path: str, device="cpu") -> Dict[str, torch.Tensor]:
+    from safetensors.torch import load_file
+    cfg = OrpheusConfig.from_hf(path)
+    sd = {}
+    for f in sorted(glob.glob(os.path.join(path, "*.safetensors"))):
+        sd.update(load_file(f, device=str(device)))
+    m = {"model.embed_tokens.weight": "embed", "model.norm.weight": "norm",
+         "lm_head.weight": "lm_head"}
+    for i in range(cfg.layers):
+        a, p = f"model.layers.{i}.", f"l{i}."
+        m.update({a + "input_layernorm.weight": p + "attn_norm",
+                  a + "post_attention_layernorm.weight": p + "mlp_norm",
+                  a + "self_attn.q_proj.weight": p + "wq", a + "self_attn.k_proj.weight": p + "wk",
+                  a + "self_attn.v_proj.weight": p + "wv", a + "self_attn.o_proj.weight": p + "wo",
+                  a + "mlp.gate_proj.weight": p + "wg", a + "mlp.up_proj.weight": p + "wu",
+                  a + "mlp.down_proj.weight": p + "wd"})
+    out = {m[k]: v for k, v in sd.items() if k in m}
+    if cfg.tied:
+        out.pop("lm_head", None)
+    missing = set(llm_shapes(cfg)) - set(out)
+    if missing:
+        raise ValueError(f"checkpoint {path} lacks {sorted(missing)[:5]}...")
+    return out
+
+
+# ------------------------------------------------------------------------------------ SNAC
+def snac_shapes() -> Dict[str, tuple]:
+    s = {}
+    for i in range(3):
+        s[f"q{i}.codebook"] = (4096, 8)
+        s[f"q{i}.out_proj.w"] = (768, 8)
+        s[f"q{i}.out_proj.b"] = (768,)
+    s.update({"in.dw.w": (768, 1, 7), "in.dw.b": (768,), "in.pw.w": (1024, 768),
+              "in.pw.b": (1024,)})
+    for b, r in enumerate(SNAC_RATES):
+        cin = 1024 >> b
+        co = cin // 2
+        p = f"b{b}."
+        s.update({p + "alpha": (cin,), p + "up.w": (cin, co, 2 * r), p + "up.b": (co,),
+                  p + "noise.w": (co, co)})
+        for j in range(3):
+            q = f"{p}r{j}."
+            s.update({q + "alpha1": (co,), q + "dw.w": (co, 1, 7), q + "dw.b": (co,),
+                      q + "alpha2": (co,), q + "pw.w": (co, co), q + "pw.b": (co,)})
+    s.update({"out.alpha": (64,), "out.conv.w": (1, 64, 7), "out.conv.b": (1,)})
+    return s
+
+
+def synthetic_snac_weights(seed: int = 3) -> Dict[str, torch.Tensor]:
+    """fp32 CPU weights with fan-in scaling so activations stay O(1) through the stack."""
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for name, shape in snac_shapes().items():
+        leaf = name.rsplit(".", 1)[-1]
+        if "alpha" in leaf:
+            w = 1.0 + 0.5 * torch.rand(shape, generator=g)
+        elif name.endswith("codebook"):
+            w = torch.randn(shape, generator=g)
+        elif leaf == "b":
+            w = 0.02 * torch.randn(shape, generator=g)
+        else:
+            fan_in = math.prod(shape[1:]) if ".up.w" not in name else shape[0] * 2
+            gain = 0.3 if "noise" in name else 1.0
+            w = gain * torch.randn(shape, generator=g) / math.sqrt(fan_in)
+        out[name] = w.float().contiguous()
+    return out
+
+
+def fold_weight_norm(g: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    dims = tuple(range(1, v.dim()))
+    return (g * v / v.norm(dim=dims, keepdim=True)).float()
+
+
+def load_snac_state_dict(path: str) -> Dict[str, torch.Tensor]:
+    """Map a snac 1.2.x SNAC state dict (24 kHz) onto the build's SNAC weight names."""
+    if os.path.isdir(path):
+        cand = glob.glob(os.path.join(path, "*.safetensors")) + \
+            glob.glob(os.path.join(path, "*.bin")) + glob.glob(os.path.join(path, "*.pt"))
+        if not cand:
+            raise FileNotFoundError(f"no SNAC checkpoint under {path}")
+        path = cand[0]
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(path)
+    else:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+
+    def w(prefix):
+        for gk, vk in ((prefix + ".weight_g", prefix + ".weight_v"),
+                       (prefix + ".parametrizations.weight.original0",
+                        prefix + ".parametrizations.weight.original1")):
+            if gk in sd:
+                return fold_weight_norm(sd[gk], sd[vk])
+        return sd[prefix + ".weight"].float()
+
+    out = {}
+    for i in range(3):
+        q = f"quantizer.quantizers.{i}."
+        out[f"q{i}.codebook"] = sd[q + "codebook.weight"].float()
+        out[f"q{i}.out_proj.w"] = w(q + "out_proj").reshape(768, 8)
+        out[f"q{i}.out_proj.b"] = sd[q + "out_proj.bias"].float()
+    d = "decoder.model."
+    out["in.dw.w"] = w(d + "0")
+    out["in.dw.b"] = sd[d + "0.bias"].float()
+    out["in.pw.w"] = w(d + "1").reshape(1024, 768)
+    out["in.pw.b"] = sd[d + "1.bias"].float()
+    for b in range(4):
+        m = f"{d}{2 + b}.block."
+        p = f"b{b}."
+        co = 512 >> b
+        out[p + "alpha"] = sd[m + "0.alpha"].float().reshape(-1)
+        out[p + "up.w"] = w(m + "1")
+        out[p + "up.b"] = sd[m + "1.bias"].float()
+        out[p + "noise.w"] = w(m + "2.linear").reshape(co, co)
+        for j in range(3):
+            r = f"{m}{3 + j}.block."
+            q = f"{p}r{j}."
+            out[q + "alpha1"] = sd[r + "0.alpha"].float().reshape(-1)
+            out[q + "dw.w"] = w(r + "1")
+            out[q + "dw.b"] = sd[r + "1.bias"].float()
+            out[q + "alpha2"] = sd[r + "2.alpha"].float().reshape(-1)
+            out[q + "pw.w"] = w(r + "3").reshape(co, co)
+            out[q + "pw.b"] = sd[r + "3.bias"].float()
+    out["out.alpha"] = sd[d + "6.alpha"].float().reshape(-1)
+    out["out.conv.w"] = w(d + "7")
+    out["out.conv.b"] = sd[d + "7.bias"].float()
+    shapes = snac_shapes()
+    for k, v in out.items():
+        if tuple(v.shape) != shapes[k]:
+            raise ValueError(f"SNAC {k}: shape {tuple(v.shape)} != {shapes[k]}")
+    return out
