@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <string>
@@ -19,6 +20,7 @@ using namespace mx;
   do {                                                                                 \
     hipError_t e_ = (expr);                                                            \
     if (e_ != hipSuccess) {                                                            \
+      (void)hipGetLastError(); /* do not leave the error for the caller's runtime */  \
       (ctx)->err = std::string(#expr) + " -> " + hipGetErrorString(e_);               \
       return MX_ERR_HIP;                                                               \
     }                                                                                  \
@@ -197,8 +199,9 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess)
     e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
-  if (e == hipSuccess) e = gemv_prepare();
+  if (e == hipSuccess) e = gemv_prepare(std::max(std::max(c.hidden, c.ffn), c.heads * 128));
   if (e != hipSuccess) {
+    (void)hipGetLastError();
     g_err = std::string("init failed: ") + hipGetErrorString(e);
     mx_llm_destroy(x);
     return MX_ERR_HIP;

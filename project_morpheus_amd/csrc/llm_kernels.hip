@@ -416,15 +416,20 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-// Allow > 64 KiB of dynamic LDS (RT = 4 tiles at K = 8192 stage 128 KiB).  Called once,
-// outside any graph capture.
-hipError_t gemv_prepare() {
-  const int bytes = 160 * 1024;
+// Allow > 64 KiB of dynamic LDS where an instantiation needs it (RT = 4 tiles at
+// K = ffn stage RT*K*4 bytes).  The request is sized per instantiation: dynamic + static
+// LDS must stay within the 160 KiB of a CU, so asking for the whole 160 KiB on a kernel
+// that also declares static __shared__ (the argmax epilogue) is rejected.  Called once per
+// context, outside any graph capture.
+hipError_t gemv_prepare(int kmax) {
   hipError_t e = hipSuccess;
-#define MX_A(RT_, RPW_, EPI_, NORM_)                                                        \
-  if (e == hipSuccess)                                                                     \
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<RT_, RPW_, EPI_, NORM_>), \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define MX_A(RT_, RPW_, EPI_, NORM_)                                                          \
+  if (e == hipSuccess) {                                                                      \
+    const int need = RT_ * kmax * 4 + 64;                                                     \
+    if (need > 64 * 1024)                                                                     \
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<RT_, RPW_, EPI_, NORM_>), \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, need);              \
+  }
   MX_A(1, 2, EPI_STORE, false) MX_A(1, 2, EPI_STORE, true)
   MX_A(1, 2, EPI_RESID, false) MX_A(1, 2, EPI_SILU, true)
   MX_A(1, 2, EPI_QKV, true) MX_A(1, 4, EPI_ARGMAX, true)

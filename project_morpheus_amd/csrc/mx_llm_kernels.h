@@ -63,7 +63,7 @@ struct CommitArgs {
   int hidden, vocab, max_pos, pos_advance;
 };
 
-hipError_t gemv_prepare();
+hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);

@@ -57,7 +57,8 @@ def test_snac_window_parity(snac_pair, n_frames, B):
         assert np.abs(audio[b] - want).max() < 1e-3
         ref_pcm = (want[2048:4096] * np.float32(32767)).astype(np.int16)
         assert pcm[b].shape == ref_pcm.shape
-        assert np.abs(pcm[b].astype(np.int32) - ref_pcm).max() <= 1
+        if ref_pcm.size:  # a 1-frame window's [2048:4096] slice is empty (speechpipe.py:122)
+            assert np.abs(pcm[b].astype(np.int32) - ref_pcm).max() <= 1
 
 
 def test_snac_audio_is_nontrivial(snac_pair):
