@@ -154,16 +154,17 @@ def main():
         firsts = [x for r in fl for x in r]
 
     # ---- roofline of the dominant kernel (gate/up GEMV: 2*ffn*hidden bf16 per launch) ----
+    # eager steps with HIP events on the engine's own stream around every launch
     st = syn.stream
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(3):
         llm.decode(1, 1.1, st)
-    ms_sum, n_launch = 0.0, 0
+    prof = {}
     for _ in range(args.profile_steps):
-        m, n = llm.decode_profiled(1, 1.1, st)
-        ms_sum += m
-        n_launch += n
-    gu_ms = ms_sum / max(1, n_launch)
+        for k, v in llm.decode_profiled(1, 1.1, st).items():
+            prof[k] = prof.get(k, 0.0) + v
+    per_step_us = {k: round(1e3 * v / args.profile_steps, 2) for k, v in prof.items()}
+    gu_ms = prof["gate_up"] / (args.profile_steps * cfg.layers)
     gu_bytes = 2 * cfg.ffn * cfg.hidden * 2
     gu_gbs = gu_bytes / (gu_ms * 1e-3) / 1e9
     # pure decode step (graph replay, no SNAC) against the whole-step byte roofline
@@ -205,6 +206,7 @@ def main():
                          "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
                          "avg_launch_us": round(gu_ms * 1e3, 3), "bytes_per_launch": gu_bytes,
                          "traffic": None},
+            "eager_step_us_by_kernel": per_step_us,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, prompt)

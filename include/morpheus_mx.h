@@ -71,10 +71,21 @@ int mx_llm_prefill(mx_llm* ctx, int slot, int row, const int32_t* ids_host, int 
                    float penalty, void* stream);
 /* One greedy decode step for rows [0, n_rows) (hipGraph-captured per n_rows; replayed). */
 int mx_llm_decode(mx_llm* ctx, int n_rows, float penalty, void* stream);
-/* Same step launched eagerly with HIP events around each gate/up GEMV; adds the kernels'
- * elapsed milliseconds to *gate_up_ms and their count to *n_launches (synchronises). */
+/* Same step launched eagerly (no graph) with HIP events around every launch; adds the
+ * elapsed milliseconds per launch class to ms_by_class[k] (k < n_classes; classes:
+ * 0 qkv, 1 attention, 2 o-proj, 3 gate/up, 4 down, 5 lm_head+argmax, 6 commit).
+ * Synchronises the stream.  Used by bench.py for the roofline of individual kernels. */
 int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, float penalty, void* stream,
-                           double* gate_up_ms, int* n_launches);
+                           double* ms_by_class, int n_classes);
+/* Tuning knobs ("legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "att_cpw",
+ * "att_cpw_batch"; see capi.hip).  Drops the
+ * captured graphs so the next mx_llm_decode re-captures with the new choice. */
+int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
+/* Diagnostic: mean microseconds of one eager attention launch (layer 0) for n_rows rows of
+ * length L, `cpw` 32-position chunks per wave (split = 128*cpw), experiment flags `debug`
+ * (0 = product kernel).  Clobbers decode-row state: only on an idle context. */
+int mx_llm_bench_attention(mx_llm* ctx, int L, int n_rows, int cpw, int debug, int reps,
+                           float* us_out);
 /* Park decode row `row` on the scratch slot (stream ended / barge-in reset). */
 int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
 /* Host-mapped token history [max_slots][max_pos] int32 written by the device. */

@@ -149,8 +149,12 @@ def apply_penalty(logits: torch.Tensor, seen: Sequence[int], penalty: float) -> 
 
 def greedy_generate(model: LlamaRef, prompt: Sequence[int], n_steps: int,
                     penalty: float = 1.1, slot: int = 0, stop_ids=(),
-                    return_logits: bool = False):
-    """Prefill ``prompt`` then ``n_steps`` greedy steps; returns generated ids."""
+                    return_logits: bool = False, forced: Optional[Sequence[int]] = None):
+    """Prefill ``prompt`` then ``n_steps`` greedy steps; returns generated ids.
+
+    ``forced`` (teacher forcing, parity harness only): feed ``forced[k]`` as the k-th
+    generated token instead of the oracle's own argmax, so the logits of every later step
+    can still be compared after a near-tie flipped one argmax."""
     model.free(slot)
     seen = list(prompt)
     logits = model.forward(list(prompt), [slot] * len(prompt), list(range(len(prompt))))[-1]
@@ -160,6 +164,8 @@ def greedy_generate(model: LlamaRef, prompt: Sequence[int], n_steps: int,
     for _ in range(n_steps):
         pl = apply_penalty(logits, seen, penalty)
         nxt = int(torch.argmax(pl))
+        if forced is not None and len(out) < len(forced):
+            nxt = int(forced[len(out)])
         if return_logits:
             trace.append(pl)
         out.append(nxt)

@@ -47,7 +47,10 @@ _SIGS = {
     "mx_llm_prefill": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int, C.c_float, _P]),
     "mx_llm_decode": (C.c_int, [_P, C.c_int, C.c_float, _P]),
     "mx_llm_decode_profiled": (C.c_int, [_P, C.c_int, C.c_float, _P,
-                                         C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+                                         C.POINTER(C.c_double), C.c_int]),
+    "mx_llm_set_option": (C.c_int, [_P, C.c_char_p, C.c_int]),
+    "mx_llm_bench_attention": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(C.c_float)]),
     "mx_llm_release_row": (C.c_int, [_P, C.c_int, _P]),
     "mx_llm_history": (C.POINTER(C.c_int32), [_P]),
     "mx_llm_debug_logits": (C.c_int, [_P, C.c_int]),

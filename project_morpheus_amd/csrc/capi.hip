@@ -85,6 +85,7 @@ struct mx_llm {
   size_t kv_layer_elems = 0;
   float *h_dec = nullptr, *h_pre = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   float *part_ml = nullptr, *part_acc = nullptr;
+  int* att_cnt = nullptr;
   int nsplit_max = 0;
   int32_t *row_slot = nullptr, *row_pos = nullptr, *row_token = nullptr;
   int32_t *pre_slot = nullptr, *pre_pos = nullptr, *pre_ids = nullptr;
@@ -95,11 +96,18 @@ struct mx_llm {
   int32_t* hist_host = nullptr;
   int32_t* hist_dev = nullptr;
   hipStream_t cap = nullptr;
-  std::map<int, hipGraphExec_t> graphs;
+  std::map<int, hipGraphExec_t> graphs;   // key: n_rows * 4096 + attention splits
+  std::vector<int> pos_mirror;            // host copy of row_pos (position of next token)
+  std::vector<char> row_active;
   std::map<int, hipGraph_t> graph_defs;
   bool final = false;
   int max_rows = 0;
   float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
+  int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
+  int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
+  int att_cpw_batch = 2;        // option: same for multi-row (batched decode / prefill)
+  int gemv_wpb = 4;             // option: waves per block of the single-row GEMV
+  int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
 
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -128,12 +136,14 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (c.hidden % 256 || c.ffn % 256) return bad("hidden and ffn must be multiples of 256");
   if (c.heads % c.kv_heads || c.heads / c.kv_heads > ATT_MAXG) return bad("bad GQA grouping");
   if (c.heads * 128 % 256) return bad("heads*128 must be a multiple of 256");
-  if (c.max_pos % ATT_CHUNK) return bad("max_pos must be a multiple of 64");
+  if (c.max_pos % 128) return bad("max_pos must be a multiple of 128");
   if (c.max_batch < 1 || c.max_prefill < 1 || c.max_slots < 1) return bad("bad limits");
   if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed");
   x->L.resize(c.layers);
+  x->pos_mirror.assign(c.max_batch, 0);
+  x->row_active.assign(c.max_batch, 0);
   x->max_rows = c.max_batch > c.max_prefill ? c.max_batch : c.max_prefill;
-  x->nsplit_max = c.max_pos / ATT_CHUNK;
+  x->nsplit_max = c.max_pos / ATT_S_MIN;
   const int qkv_rows = c.heads * 128 + 2 * c.kv_heads * 128;
   const int slots = c.max_slots + 1;  // +1 scratch slot for parked rows
   x->kv_layer_elems = (size_t)slots * c.kv_heads * c.max_pos * 128;
@@ -158,8 +168,11 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->q, (size_t)x->max_rows * c.heads * 128);
   A(x->att, (size_t)x->max_rows * c.heads * 128);
   A(x->act, (size_t)x->max_rows * c.ffn);
-  A(x->part_ml, (size_t)x->max_rows * c.heads * x->nsplit_max * 2);
-  A(x->part_acc, (size_t)x->max_rows * c.heads * x->nsplit_max * 128);
+  // split partials: prefill rows use 128-position splits, decode rows down to 32
+  const size_t part_rows = (size_t)x->max_rows * (c.max_pos / ATT_S_MIN);
+  A(x->part_ml, part_rows * c.heads * 2);
+  A(x->part_acc, part_rows * c.heads * 128);
+  A(x->att_cnt, (size_t)x->max_rows * c.kv_heads);
   A(x->row_slot, c.max_batch);
   A(x->row_pos, c.max_batch);
   A(x->row_token, c.max_batch);
@@ -190,6 +203,7 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   e = hipMemset(x->kcache, 0, x->kv_layer_elems * c.layers * 2);
   if (e == hipSuccess) e = hipMemset(x->vcache, 0, x->kv_layer_elems * c.layers * 2);
   if (e == hipSuccess) e = hipMemset(x->best, 0, c.max_batch * 8);
+  if (e == hipSuccess) e = hipMemset(x->att_cnt, 0, (size_t)x->max_rows * c.kv_heads * 4);
   if (e == hipSuccess) e = hipMemset(x->seen, 0, (size_t)slots * c.vocab);
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
   // every decode row starts parked on the scratch slot at position 0
@@ -353,10 +367,26 @@ struct RowSet {
   const int32_t* slot;
   const int32_t* pos;
   int R;
+  int max_len;  // upper bound of any row's position + 1 (sizes the attention grid)
 };
 
-static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st,
-                                 std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+// Optional per-launch timing (eager runs only): prof->ev[k] brackets launch class k.
+enum { PK_QKV = 0, PK_ATTN, PK_O, PK_GU, PK_DOWN, PK_HEAD, PK_COMMIT, PK_N };
+struct Prof {
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  void begin(int k, hipStream_t st) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, st);
+    ev.push_back({k, {a, b}});
+  }
+  void end(hipStream_t st) { (void)hipEventRecord(ev.back().second.second, st); }
+};
+#define PROF_BEGIN(k) if (prof) prof->begin(k, st)
+#define PROF_END() if (prof) prof->end(st)
+
+static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Prof* prof) {
   const auto& c = x->c;
   const int H = c.hidden, QD = c.heads * 128;
   const int qkv_rows = QD + 2 * c.kv_heads * 128;
@@ -372,40 +402,46 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st,
     g.W = l.wqkv; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
-    g.max_pos = c.max_pos; g.Q = x->q;
+    g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
+    PROF_BEGIN(PK_QKV);
     e = launch_gemv(g, EPI_QKV, true, st);
+    PROF_END();
     if (e != hipSuccess) break;
     AttnArgs at{};
     at.Q = x->q; at.kcache = kc; at.vcache = vc; at.row_slot = rs.slot; at.row_pos = rs.pos;
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
-    at.nsplit_max = x->nsplit_max; at.scale = 1.0f / sqrtf(128.0f);
-    at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.out = x->att;
-    e = launch_attention(at, rs.R, st);
+    at.scale = 1.0f / sqrtf(128.0f);
+    at.cpw = rs.R == 1 ? x->att_cpw_b1 : x->att_cpw_batch;
+    at.split_stride = c.max_pos / ATT_S_MIN;
+    at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
+    at.out = x->att;
+    PROF_BEGIN(PK_ATTN);
+    e = launch_attention(at, rs.R, rs.max_len, st);
+    PROF_END();
     if (e != hipSuccess) break;
     // O projection + residual
     GemvArgs o{};
     o.R = rs.R; o.W = l.wo; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
-    o.ystride = H;
+    o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
+    PROF_BEGIN(PK_O);
     e = launch_gemv(o, EPI_RESID, false, st);
+    PROF_END();
     if (e != hipSuccess) break;
     // gate/up + SiLU*up
     GemvArgs gu{};
     gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
-    gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act;
-    if (prof) {
-      prof->emplace_back();
-      (void)hipEventCreate(&prof->back().first);
-      (void)hipEventCreate(&prof->back().second);
-      (void)hipEventRecord(prof->back().first, st);
-    }
+    gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act; gu.force_legacy = x->legacy_gemv; gu.wpb = x->gemv_wpb; gu.rpw = x->rpw_gu;
+    PROF_BEGIN(PK_GU);
     e = launch_gemv(gu, EPI_SILU, true, st);
-    if (prof) (void)hipEventRecord(prof->back().second, st);
+    PROF_END();
     if (e != hipSuccess) break;
     // down + residual
     GemvArgs d{};
     d.R = rs.R; d.W = l.wd; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
-    d.ystride = H;
+    d.ystride = H; d.force_legacy = x->legacy_gemv; d.wpb = x->gemv_wpb; d.rpw = x->rpw_down;
+    PROF_BEGIN(PK_DOWN);
     e = launch_gemv(d, EPI_RESID, false, st);
+    PROF_END();
   }
   return e;
 }
@@ -421,20 +457,31 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot, i
   return launch_gemv(g, EPI_ARGMAX, true, st);
 }
 
-static hipError_t enqueue_decode(mx_llm* x, int n_rows, hipStream_t st,
-                                 std::vector<std::pair<hipEvent_t, hipEvent_t>>* prof) {
+// Longest attention span of the next step over rows [0, n_rows) (host mirror of row_pos).
+static int decode_max_len(const mx_llm* x, int n_rows) {
+  int m = 1;
+  for (int r = 0; r < n_rows; ++r)
+    if (x->row_active[r]) m = std::max(m, x->pos_mirror[r] + 1);
+  return m;
+}
+
+static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, hipStream_t st, Prof* prof) {
   const auto& c = x->c;
-  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows};
+  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len};
   hipError_t e = enqueue_layers(x, rs, st, prof);
+  PROF_BEGIN(PK_HEAD);
   if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, n_rows, x->best, st);
+  PROF_END();
+  PROF_BEGIN(PK_COMMIT);
   if (e == hipSuccess) {
     CommitArgs cm{};
     cm.best = x->best; cm.row_slot = x->row_slot; cm.row_pos = x->row_pos;
     cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
     cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
-    cm.pos_advance = 1;
+    cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
     e = launch_commit(cm, n_rows, st);
   }
+  PROF_END();
   return e;
 }
 
@@ -464,7 +511,7 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, launch_set_rows(x->pre_slot, x->pre_pos, n, slot, 0, st));
   MX_TRY(x, launch_embed_rows(x->pre_ids, n, slot, x->embed, c.hidden, c.vocab, x->seen,
                               x->h_pre, st));
-  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n};
+  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n};
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
   MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1), 1,
@@ -475,8 +522,23 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   cm.best = x->best + row; cm.row_slot = x->row_slot + row; cm.row_pos = x->row_pos + row;
   cm.row_token = x->row_token + row; cm.seen = x->seen; cm.hist = x->hist_dev;
   cm.embed = x->embed; cm.h = x->h_dec + (size_t)row * c.hidden; cm.hidden = c.hidden;
-  cm.vocab = c.vocab; cm.max_pos = c.max_pos; cm.pos_advance = 1;
+  cm.vocab = c.vocab; cm.max_pos = c.max_pos; cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
   MX_TRY(x, launch_commit(cm, 1, st));
+  x->pos_mirror[row] = n;
+  x->row_active[row] = 1;
+  return MX_OK;
+}
+
+// Advance the host mirror after a step over rows [0, n_rows) was enqueued.
+static void mirror_step(mx_llm* x, int n_rows) {
+  for (int r = 0; r < n_rows; ++r)
+    if (x->row_active[r]) x->pos_mirror[r] = std::min(x->pos_mirror[r] + 1, x->c.max_pos - 1);
+}
+
+static int check_room(mx_llm* x, int n_rows) {
+  for (int r = 0; r < n_rows; ++r)
+    if (x->row_active[r] && x->pos_mirror[r] >= x->c.max_pos - 1)
+      MX_FAIL(x, MX_ERR_STATE, "row " + std::to_string(r) + " reached max_pos");
   return MX_OK;
 }
 
@@ -484,51 +546,138 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   if (!x) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
+  if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
   if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
-  auto it = x->graphs.find(n_rows);
+  // one graph per (row count, attention split count): kernels read positions from device
+  // memory; the split count only sizes the attention grid
+  const int S = ATT_S_MIN * (n_rows == 1 ? x->att_cpw_b1 : x->att_cpw_batch);
+  const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
+  const int key = n_rows * 4096 + nsplit;
+  auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
-    // capture on the private stream; kernels read row positions from device memory so
-    // one graph serves every step
     MX_TRY(x, hipStreamSynchronize(st));
     MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
-    hipError_t e = enqueue_decode(x, n_rows, x->cap, nullptr);
+    hipError_t e = enqueue_decode(x, n_rows, nsplit * S, x->cap, nullptr);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(x->cap, &g);
     MX_TRY(x, e);
     MX_TRY(x, e2);
     hipGraphExec_t ex = nullptr;
     MX_TRY(x, hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    x->graph_defs[n_rows] = g;
-    it = x->graphs.emplace(n_rows, ex).first;
+    x->graph_defs[key] = g;
+    it = x->graphs.emplace(key, ex).first;
   }
   MX_TRY(x, hipGraphLaunch(it->second, st));
+  mirror_step(x, n_rows);
   return MX_OK;
 }
 
 extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, float penalty, void* stream,
-                                      double* gate_up_ms, int* n_launches) {
-  if (!x) return MX_ERR_ARG;
+                                      double* ms_by_class, int n_classes) {
+  if (!x || !ms_by_class) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
   if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
-  hipError_t e = enqueue_decode(x, n_rows, st, &ev);
+  if (check_room(x, n_rows)) return MX_ERR_STATE;
+  Prof prof;
+  hipError_t e = enqueue_decode(x, n_rows, decode_max_len(x, n_rows), st, &prof);
+  mirror_step(x, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  double tot = 0.0;
-  for (auto& p : ev) {
+  for (auto& p : prof.ev) {
     float ms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, p.first, p.second);
-    tot += ms;
-    (void)hipEventDestroy(p.first);
-    (void)hipEventDestroy(p.second);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, p.second.first, p.second.second);
+    if (p.first < n_classes) ms_by_class[p.first] += ms;
+    (void)hipEventDestroy(p.second.first);
+    (void)hipEventDestroy(p.second.second);
   }
   MX_TRY(x, e);
-  if (gate_up_ms) *gate_up_ms += tot;
-  if (n_launches) *n_launches += (int)ev.size();
+  return MX_OK;
+}
+
+// Diagnostic: time `reps` launches of layer 0's attention, captured in one hipGraph (so
+// host launch rate does not floor the measurement), for n_rows rows of length L; row i
+// uses KV slot i % max_slots (KV contents are irrelevant to the timing).  Writes the mean
+// microseconds per launch, inter-kernel gap included.  Clobbers decode-row state: call on
+// an idle context only.
+extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int debug,
+                                      int reps, float* us_out) {
+  if (!x || !us_out || L < 1 || L > x->c.max_pos || n_rows < 1 || n_rows > x->c.max_batch ||
+      reps < 1)
+    return MX_ERR_ARG;
+  const auto& c = x->c;
+  MX_TRY(x, hipSetDevice(x->device));
+  hipStream_t st = x->cap;
+  std::vector<int32_t> slots(n_rows), pos(n_rows, L - 1);
+  for (int i = 0; i < n_rows; ++i) slots[i] = i % c.max_slots;
+  MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
+  MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
+  AttnArgs at{};
+  at.Q = x->q; at.kcache = x->kcache; at.vcache = x->vcache; at.row_slot = x->row_slot;
+  at.row_pos = x->row_pos; at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
+  at.scale = 1.0f / sqrtf(128.0f); at.cpw = cpw; at.split_stride = c.max_pos / ATT_S_MIN;
+  at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt; at.out = x->att;
+  at.debug = debug;
+  MX_TRY(x, launch_attention(at, n_rows, L, st));  // warm + argument check
+  MX_TRY(x, hipStreamSynchronize(st));
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  MX_TRY(x, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < reps && e == hipSuccess; ++i) e = launch_attention(at, n_rows, L, st);
+  hipError_t e2 = hipStreamEndCapture(st, &g);
+  MX_TRY(x, e);
+  MX_TRY(x, e2);
+  MX_TRY(x, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  hipEvent_t e0, e1;
+  MX_TRY(x, hipEventCreate(&e0));
+  MX_TRY(x, hipEventCreate(&e1));
+  MX_TRY(x, hipGraphLaunch(ge, st));  // warm replay
+  MX_TRY(x, hipEventRecord(e0, st));
+  MX_TRY(x, hipGraphLaunch(ge, st));
+  MX_TRY(x, hipEventRecord(e1, st));
+  MX_TRY(x, hipEventSynchronize(e1));
+  float ms = 0.f;
+  MX_TRY(x, hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipGraphExecDestroy(ge);
+  (void)hipGraphDestroy(g);
+  // park the rows again
+  MX_TRY(x, launch_set_rows(x->row_slot, x->row_pos, n_rows, c.max_slots, 0, st));
+  MX_TRY(x, hipStreamSynchronize(st));
+  *us_out = 1e3f * ms / reps;
+  return MX_OK;
+}
+
+extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
+  if (!x || !key) return MX_ERR_ARG;
+  const std::string k(key);
+  if (k == "legacy_gemv") {
+    x->legacy_gemv = value;
+  } else if (k == "gemv_wpb") {
+    if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "gemv_wpb must be 4 or 8");
+    x->gemv_wpb = value;
+  } else if (k == "rpw_o" || k == "rpw_down") {
+    if (value != 0 && value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rpw must be 0, 1 or 2");
+    (k == "rpw_o" ? x->rpw_o : x->rpw_down) = value;
+  } else if (k == "rpw_gu") {
+    if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
+    x->rpw_gu = value;
+  } else if (k == "att_cpw" || k == "att_cpw_batch") {
+    if (value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4");
+    (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
+  } else {
+    MX_FAIL(x, MX_ERR_ARG, "unknown option " + k);
+  }
+  // captured graphs baked the old choice in: drop them
+  for (auto& kv : x->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : x->graph_defs) (void)hipGraphDestroy(kv.second);
+  x->graphs.clear();
+  x->graph_defs.clear();
   return MX_OK;
 }
 
@@ -537,6 +686,8 @@ extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
   MX_TRY(x, hipSetDevice(x->device));
   MX_TRY(x, launch_set_rows(x->row_slot + row, x->row_pos + row, 1, x->c.max_slots, 0,
                             (hipStream_t)stream));
+  x->pos_mirror[row] = 0;
+  x->row_active[row] = 0;
   return MX_OK;
 }
 

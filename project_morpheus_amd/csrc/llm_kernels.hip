@@ -174,10 +174,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
                 k[p + 64] = f32_to_bf16(o2);
               }
             } else {
+              // V cache is stored transposed, [slot][kv_head][dim][pos] (see attn_kernel)
               uint16_t* v = a.vcache +
-                  (((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * a.max_pos + pos) * 128;
-              v[within] = f32_to_bf16(x1);
-              v[within + 1] = f32_to_bf16(x2);
+                  ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
+              v[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
+              v[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
             }
           }
         }
@@ -201,92 +202,418 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// Split-KV decode attention, GQA group of (heads / kv_heads) q-heads per kv-head.
-// Grid (nsplit, kv_heads, R); block 256.  Split = ATT_CHUNK positions.
-// K rows are 256 contiguous bytes: 16 lanes x 16 B per position, 4 positions per
-// wave-instruction.  Partial (m, l, acc[128]) per (row, q-head, split).
+// Single-row (B = 1 decode) weight-streaming GEMV.
+//   One wave owns RPW consecutive weight rows over the whole K = 512*KCH; 8 waves per
+//   block share one LDS copy of the (RMS-normalised) activation row.  Load order is the
+//   point (cdna_hip_programming.md §5 row "GEMV / M <= 16"): the activation / norm loads
+//   go first, then every weight load of the wave (RPW*KCH x 16 B per lane, non-temporal),
+//   and only then the prologue (norm, LDS staging) runs, under the weight loads' latency.
+//   All loads are unconditional (addresses clamped), so hipcc can count vmcnt exactly.
+//   Epilogue operands that do not depend on the result (residual, RoPE row) are fetched
+//   with the activation.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a) {
-  const int split = blockIdx.x, kvh = blockIdx.y, r = blockIdx.z;
-  const int pos = a.row_pos[r], L = pos + 1;
-  const int s0 = split * ATT_CHUNK;
-  if (s0 >= L) return;
-  const int n = min(ATT_CHUNK, L - s0);
-  const int slot = a.row_slot[r];
+template <int KCH, int RPW, int EPI, bool NORM, int WPB>
+__global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
+  constexpr int NT = WPB * 64;
+  constexpr int K8 = KCH * 64;                 // 16-byte weight chunks per row
+  constexpr int XPT = (K8 + NT - 1) / NT;      // activation chunks per thread
+  __shared__ __attribute__((aligned(16))) float4 xs[2 * K8];  // lo plane | hi plane
+  __shared__ float red[WPB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int grp = a.heads / a.kv_heads;  // 3 for Orpheus
-  __shared__ __attribute__((aligned(16))) float qs[ATT_MAXG][128];
-  __shared__ float sc[ATT_MAXG][ATT_CHUNK];
+  const int G = a.N / RPW;
+  int g = blockIdx.x * WPB + wid;
+  const bool active = g < G;
+  g = active ? g : G - 1;
+  const int n0 = g * RPW;
 
-  for (int i = tid; i < grp * 128; i += 256)
-    qs[i >> 7][i & 127] = a.Q[((size_t)r * a.heads + kvh * grp) * 128 + i];
-  __syncthreads();
-
-  const size_t base = ((size_t)slot * a.kv_heads + kvh) * a.max_pos;
-  const uint16_t* K = a.kcache + base * 128;
-  const uint16_t* V = a.vcache + base * 128;
-  const int sub = lane >> 4, d8 = (lane & 15) * 8;
-  const float scale = a.scale;
-  // scores: wave wid covers positions [wid*16, wid*16+16) of the chunk
+  // 1. activation (+ norm weight, + epilogue operands)
+  const float4* X4 = reinterpret_cast<const float4*>(a.X);
+  const float4* NW4 = reinterpret_cast<const float4*>(a.norm_w);
+  float4 xl[XPT], xh[XPT], nl[XPT], nh[XPT];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int j = wid * 16 + it * 4 + sub;
-    const bool ok = j < n;
-    uint4 kv = make_uint4(0, 0, 0, 0);
-    if (ok) kv = *reinterpret_cast<const uint4*>(K + (size_t)(s0 + j) * 128 + d8);
-    for (int h = 0; h < grp; ++h) {
-      const float4 lo = *reinterpret_cast<const float4*>(&qs[h][d8]);
-      const float4 hi = *reinterpret_cast<const float4*>(&qs[h][d8 + 4]);
-      float d = dot8(kv, lo, hi, 0.f);
-      d = group_sum<16>(d);
-      if ((lane & 15) == 0) sc[h][j] = ok ? d * scale : -INFINITY;
+  for (int i = 0; i < XPT; ++i) {
+    const int c8 = min(tid + i * NT, K8 - 1);
+    xl[i] = X4[2 * c8];
+    xh[i] = X4[2 * c8 + 1];
+    if (NORM) {
+      nl[i] = NW4[2 * c8];
+      nh[i] = NW4[2 * c8 + 1];
+    }
+  }
+  float res[RPW];
+  if (EPI == EPI_RESID) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) res[r] = a.Y[n0 + r];
+  }
+  // 2. every weight load of this wave
+  uint4 w[RPW][KCH];
+  const uint4* wp = reinterpret_cast<const uint4*>(a.W) + (size_t)n0 * K8 + lane;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) w[r][c] = load_nt(wp + (size_t)r * K8 + c * 64);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // 3. prologue under the weight latency
+  float scale = 1.f;
+  if (NORM) {
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      if (tid + i * NT < K8) {
+        ss += xl[i].x * xl[i].x + xl[i].y * xl[i].y + xl[i].z * xl[i].z + xl[i].w * xl[i].w;
+        ss += xh[i].x * xh[i].x + xh[i].y * xh[i].y + xh[i].z * xh[i].z + xh[i].w * xh[i].w;
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wid] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < WPB; ++i) tot += red[i];
+    scale = 1.0f / sqrtf(tot / (float)(K8 * 8) + a.eps);
+  }
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int c8 = tid + i * NT;
+    if (c8 < K8) {
+      float4 lo = xl[i], hi = xh[i];
+      if (NORM) {
+        lo.x = lo.x * scale * nl[i].x; lo.y = lo.y * scale * nl[i].y;
+        lo.z = lo.z * scale * nl[i].z; lo.w = lo.w * scale * nl[i].w;
+        hi.x = hi.x * scale * nh[i].x; hi.y = hi.y * scale * nh[i].y;
+        hi.z = hi.z * scale * nh[i].z; hi.w = hi.w * scale * nh[i].w;
+      }
+      xs[c8] = lo;
+      xs[K8 + c8] = hi;
     }
   }
   __syncthreads();
-  // softmax partial per head (wave h handles head h; 64 lanes <-> 64 positions)
-  if (wid < grp) {
-    const float v = sc[wid][lane];
-    const float m = wave_max(v);
-    const float e = lane < n ? expf(v - m) : 0.f;
-    const float l = wave_sum(e);
-    sc[wid][lane] = e;
-    if (lane == 0) {
-      float* ml = a.part_ml + (((size_t)r * a.heads + kvh * grp + wid) * a.nsplit_max + split) * 2;
-      ml[0] = m;
-      ml[1] = l;
-    }
+
+  // 4. dot products (fp32 accumulate), wave butterfly
+  float acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const float4 lo = xs[c * 64 + lane], hi = xs[K8 + c * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) acc[r] = dot8(w[r][c], lo, hi, acc[r]);
   }
-  __syncthreads();
-  // P.V: wave h -> head h, lane -> two output dims (4-byte bf16x2 loads, 256 B per position)
-  if (wid < grp) {
-    float o0 = 0.f, o1 = 0.f;
-    const int d2 = lane * 2;
-    for (int j = 0; j < n; ++j) {
-      const uint32_t vv = *reinterpret_cast<const uint32_t*>(V + (size_t)(s0 + j) * 128 + d2);
-      const float p = sc[wid][j];
-      o0 = fmaf(p, bf16_lo(vv), o0);
-      o1 = fmaf(p, bf16_hi(vv), o1);
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) acc[r] = wave_sum(acc[r]);
+  if (!active || lane != 0) return;
+
+  // 5. epilogues
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) a.Y[n0 + r] = acc[r];
+  } else if (EPI == EPI_RESID) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) a.Y[n0 + r] = res[r] + acc[r];
+  } else if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int r = 0; r < RPW; r += 2) {
+      const float gt = acc[r], up = acc[r + 1];
+      a.Y[(n0 + r) >> 1] = gt / (1.0f + expf(-gt)) * up;
     }
-    float* acc = a.part_acc + (((size_t)r * a.heads + kvh * grp + wid) * a.nsplit_max + split) * 128;
-    *reinterpret_cast<float2*>(acc + d2) = make_float2(o0, o1);
+  } else if (EPI == EPI_QKV) {
+    const int slot = a.row_slot[0], pos = a.row_pos[0];
+#pragma unroll
+    for (int r = 0; r < RPW; r += 2) {
+      const int n = n0 + r;
+      const int hh = n >> 7, within = n & 127, p = within >> 1;
+      const float x1 = acc[r], x2 = acc[r + 1];
+      if (hh < a.heads + a.kv_heads) {
+        const float cs = a.rope_cos[(size_t)pos * 64 + p];
+        const float sn = a.rope_sin[(size_t)pos * 64 + p];
+        const float o1 = x1 * cs - x2 * sn;
+        const float o2 = x2 * cs + x1 * sn;
+        if (hh < a.heads) {
+          float* q = a.Q + (size_t)hh * 128;
+          q[p] = o1;
+          q[p + 64] = o2;
+        } else {
+          uint16_t* k = a.kcache + (((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos + pos) * 128;
+          k[p] = f32_to_bf16(o1);
+          k[p + 64] = f32_to_bf16(o2);
+        }
+      } else {
+        uint16_t* v = a.vcache +
+            ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
+        v[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
+        v[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
+      }
+    }
   }
 }
 
-// Combine split partials -> attention output row [heads*128].  Grid (heads, R), block 128.
-__global__ __launch_bounds__(128) void attn_combine_kernel(AttnArgs a) {
-  const int h = blockIdx.x, r = blockIdx.y, d = threadIdx.x;
-  const int L = a.row_pos[r] + 1;
-  const int ns = (L + ATT_CHUNK - 1) / ATT_CHUNK;
-  const size_t b = ((size_t)r * a.heads + h) * a.nsplit_max;
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.part_ml[(b + s) * 2]);
-  float den = 0.f, num = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float w = expf(a.part_ml[(b + s) * 2] - M);
-    den = fmaf(w, a.part_ml[(b + s) * 2 + 1], den);
-    num = fmaf(w, a.part_acc[(b + s) * 128 + d], num);
+// ---------------------------------------------------------------------------------
+// Decode / prefill attention on bf16 MFMA, one launch: split-KV partials + in-launch merge.
+//   Grid (nsplit, kv_heads, R), block 256 = 4 waves; a wave owns CPW chunks of 32 positions
+//   (split S = 128 * CPW), streaming them with an online softmax.  Per chunk:
+//   * S^T = K Q^T with mfma_f32_16x16x32_bf16: A = K rows straight from the cache (16 B per
+//     lane), B = the GRP q-heads of this kv-head (GQA 3:1), padded to 16 columns.  Q is
+//     fp32; it enters as three bf16 parts q0 + q1 + q2 (24 mantissa bits), so the scores
+//     are the fp32 products of the oracle up to summation order.  MFMA row r of tile T
+//     holds position 8(r>>2) + 4T + (r&3): after the MFMA the lane (head h, group g) owns
+//     the scores of positions 8g .. 8g+7, which is exactly its A fragment for P.V.
+//   * O^T += P V with the same instruction: A = P (three bf16 parts, lane-local, no data
+//     movement), B = V^T fragments.  The V cache is kept TRANSPOSED ([slot][kvh][dim][pos])
+//     so a lane's B fragment (8 consecutive positions of one dim) is one 16-byte load.
+//   Waves merge in LDS; with several splits the block publishes (m, l, acc) with
+//   write-through (sc1) stores, takes a ticket on a per-(row, kv-head) counter and the last
+//   arriver merges every split with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1),
+//   then resets the counter for the next launch.
+// ---------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+// x = p0 + p1 + p2 with p_i bf16 (exact to fp32 rounding); 8 values -> three fragments
+__device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, bf16x8& f2) {
+  uint32_t w0[4], w1[4], w2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = x[2 * j], b = x[2 * j + 1];
+    const float a0 = bf16_to_f32(f32_to_bf16(a)), b0 = bf16_to_f32(f32_to_bf16(b));
+    const float a1 = a - a0, b1 = b - b0;
+    const float a1r = bf16_to_f32(f32_to_bf16(a1)), b1r = bf16_to_f32(f32_to_bf16(b1));
+    w0[j] = pack_bf16(a0, b0);
+    w1[j] = pack_bf16(a1r, b1r);
+    w2[j] = pack_bf16(a1 - a1r, b1 - b1r);
   }
-  a.out[((size_t)r * a.heads + h) * 128 + d] = num / den;
+  f0 = __builtin_bit_cast(bf16x8, make_uint4(w0[0], w0[1], w0[2], w0[3]));
+  f1 = __builtin_bit_cast(bf16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
+  f2 = __builtin_bit_cast(bf16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
+}
+
+template <int GRP, int CPW>
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  constexpr int S = 128 * CPW;
+  const int split = blockIdx.x, kvh = blockIdx.y, r = blockIdx.z;
+  const int L = a.row_pos[r] + 1;
+  const int nsplit = (L + S - 1) / S;
+  if (split >= nsplit) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int slot = a.row_slot[r];
+  const size_t head = (size_t)slot * a.kv_heads + kvh;
+  const uint4* K = reinterpret_cast<const uint4*>(a.kcache) + head * a.max_pos * 16;
+  const uint16_t* VT = a.vcache + head * 128 * a.max_pos;
+
+  // Q^T fragments: lane (col c = head, group g) holds q[c][32 s + 8 g + j], 3 bf16 parts
+  bf16x8 qf[3][4];
+  {
+    const int hq = c < GRP ? c : 0;
+    const float* qb = a.Q + ((size_t)r * a.heads + kvh * GRP + hq) * 128 + 8 * g;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      float x[8];
+      const float4 lo = *reinterpret_cast<const float4*>(qb + 32 * st);
+      const float4 hi = *reinterpret_cast<const float4*>(qb + 32 * st + 4);
+      x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w;
+      x[4] = hi.x; x[5] = hi.y; x[6] = hi.z; x[7] = hi.w;
+      if (c >= GRP) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = 0.f;
+      }
+      split3(x, qf[0][st], qf[1][st], qf[2][st]);
+    }
+  }
+
+  float M = -INFINITY, lsum = 0.f;
+  f32x4 acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rr = lane & 15;
+  for (int ch = 0; ch < CPW; ++ch) {
+    const int base = split * S + (wid * CPW + ch) * 32;
+    if (base >= L) break;  // wave-uniform
+    // K fragments (A operand): tile T, MFMA row rr -> position 8(rr>>2) + 4T + (rr&3)
+    uint4 kf[2][4];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+      const int p = min(base + 8 * (rr >> 2) + 4 * T + (rr & 3), L - 1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) kf[T][st] = K[(size_t)p * 16 + 4 * st + g];
+    }
+    // V^T fragments (B operand): lane (dim 16 t + c, group g) <- positions base + 8g .. +8
+    uint4 vf[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      vf[t] = *reinterpret_cast<const uint4*>(VT + (size_t)(16 * t + c) * a.max_pos + base + 8 * g);
+    __builtin_amdgcn_sched_barrier(0);
+    // scores
+    f32x4 sc[2];
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+      sc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const bf16x8 kb = __builtin_bit_cast(bf16x8, kf[T][st]);
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt)
+          sc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb, qf[pt][st], sc[T], 0, 0, 0);
+      }
+    }
+    // online softmax: this lane holds head c, positions base + 8g + j (j = 4T + i)
+    float s[8];
+    float mc = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = base + 8 * g + j;
+      s[j] = p < L ? sc[j >> 2][j & 3] * a.scale : -INFINITY;
+      mc = fmaxf(mc, s[j]);
+    }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    const float Mn = fmaxf(M, mc);  // finite: position base < L is in this chunk
+    const float alpha = expf(M - Mn);  // M = -inf on the first chunk -> 0
+    float pv[8], ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pv[j] = expf(s[j] - Mn);
+      ps += pv[j];
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    lsum = lsum * alpha + ps;
+    M = Mn;
+    // rescale O^T rows (row = head 4 g + i): alpha of head h lives in lane h
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float al = __shfl(alpha, (4 * g + i) & 15, 64);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t][i] *= al;
+    }
+    bf16x8 pf[3];
+    split3(pv, pf[0], pf[1], pf[2]);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const bf16x8 vb = __builtin_bit_cast(bf16x8, vf[t]);
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt], vb, acc[t], 0, 0, 0);
+    }
+  }
+
+  __shared__ __attribute__((aligned(16))) float wacc[4][GRP][128];
+  __shared__ float wml[4][GRP][2];
+  __shared__ float sml[ATT_MAX_SPLITS][GRP][2];
+  __shared__ int last_s;
+  // (M, lsum) of head c sit in lanes c (any g); O^T row h = 4 g + i, dim 16 t + c
+  if (g == 0 && c < GRP) {
+    wml[wid][c][0] = M;
+    wml[wid][c][1] = lsum;
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < GRP && i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) wacc[wid][i][16 * t + c] = acc[t][i];
+  }
+  __syncthreads();
+  // block merge: thread -> (head tid / 128 (+2), dim tid % 128)
+  const int th = tid >> 7, td = tid & 127;
+  float bm[2] = {0.f, 0.f}, bl[2] = {0.f, 0.f}, bn[2] = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int h = th + 2 * k;
+    if (h < GRP) {
+      float Mb = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) Mb = fmaxf(Mb, wml[w][h][0]);
+      float num = 0.f, den = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float mw = wml[w][h][0];
+        const float f = (mw == -INFINITY) ? 0.f : expf(mw - Mb);
+        num = fmaf(f, wacc[w][h][td], num);
+        den = fmaf(f, wml[w][h][1], den);
+      }
+      bm[k] = Mb;
+      bl[k] = den;
+      bn[k] = num;
+    }
+  }
+  float* out = a.out + ((size_t)r * a.heads + kvh * GRP) * 128;
+  if (nsplit == 1) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int h = th + 2 * k;
+      if (h < GRP) out[h * 128 + td] = bn[k] / bl[k];
+    }
+    return;
+  }
+  // publish this split's partial (write-through), then take a ticket
+  const size_t pb = ((size_t)r * a.kv_heads + kvh) * a.split_stride;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int h = th + 2 * k;
+    if (h < GRP) {
+      st_wt(a.part_acc + ((pb + split) * GRP + h) * 128 + td, bn[k]);
+      if (td == 0) {
+        st_wt(a.part_ml + ((pb + split) * GRP + h) * 2, bm[k]);
+        st_wt(a.part_ml + ((pb + split) * GRP + h) * 2 + 1, bl[k]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    int* cnt = a.counter + (size_t)r * a.kv_heads + kvh;
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == nsplit - 1);
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = last;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  // last arriver: the (m, l) pairs and this thread's accumulator column of every split are
+  // loaded in ONE round trip (ATT_MERGE_CHUNK splits at a time), then merged.
+  for (int i = tid; i < nsplit * GRP * 2; i += 256)
+    (&sml[0][0][0])[i] = ld_wt(a.part_ml + pb * GRP * 2 + i);
+  float col[2][ATT_MERGE_CHUNK];
+  const int n0 = min(nsplit, ATT_MERGE_CHUNK);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int h = min(th + 2 * k, GRP - 1);
+#pragma unroll
+    for (int sp = 0; sp < ATT_MERGE_CHUNK; ++sp)
+      col[k][sp] = ld_wt(a.part_acc + ((pb + min(sp, n0 - 1)) * GRP + h) * 128 + td);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int h = th + 2 * k;
+    if (h >= GRP) continue;
+    float Mb = -INFINITY;
+    for (int sp = 0; sp < nsplit; ++sp) Mb = fmaxf(Mb, sml[sp][h][0]);
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < ATT_MERGE_CHUNK; ++sp) {
+      if (sp < n0) {
+        const float f = expf(sml[sp][h][0] - Mb);
+        num = fmaf(f, col[k][sp], num);
+        den = fmaf(f, sml[sp][h][1], den);
+      }
+    }
+    for (int sp = ATT_MERGE_CHUNK; sp < nsplit; ++sp) {  // long contexts only
+      const float f = expf(sml[sp][h][0] - Mb);
+      num = fmaf(f, ld_wt(a.part_acc + ((pb + sp) * GRP + h) * 128 + td), num);
+      den = fmaf(f, sml[sp][h][1], den);
+    }
+    out[h * 128 + td] = num / den;
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -303,11 +630,13 @@ __global__ __launch_bounds__(256) void commit_kernel(CommitArgs a) {
     tok_s = tok;
     a.best[r] = 0ull;
     const int slot = a.row_slot[dst];
-    const int pos = a.row_pos[dst] + a.pos_advance;  // position of the new token
-    a.row_pos[dst] = pos;
-    a.row_token[dst] = tok;
-    a.seen[(size_t)slot * a.vocab + tok] = 1;
-    if (pos < a.max_pos) a.hist[(size_t)slot * a.max_pos + pos] = tok;
+    if (slot != a.scratch_slot) {  // parked rows stay at position 0 of the scratch slot
+      const int pos = min(a.row_pos[dst] + a.pos_advance, a.max_pos - 1);  // new token
+      a.row_pos[dst] = pos;
+      a.row_token[dst] = tok;
+      a.seen[(size_t)slot * a.vocab + tok] = 1;
+      a.hist[(size_t)slot * a.max_pos + pos] = tok;
+    }
   }
   __syncthreads();
   const int tok = tok_s;
@@ -397,7 +726,42 @@ static int gemv_blocks(int N, int rpw, int ytiles, int target) {
   return b < cap ? b : (cap > 0 ? cap : 1);
 }
 
+template <int KCH, int RPW, int EPI, bool NORM>
+static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
+  const int G = a.N / RPW;
+  if (a.wpb == 4)
+    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 4>), dim3((G + 3) / 4), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8>), dim3((G + 7) / 8), dim3(512), 0, st, a);
+  return hipGetLastError();
+}
+
+// B = 1 path; returns hipErrorNotSupported when the shape has no instantiation.
+// a.rpw (0 = default per epilogue) picks rows per wave: QKV 2, RESID/STORE 1, SILU 4|2.
+static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
+  if (a.K % 512) return hipErrorNotSupported;
+  const int kch = a.K / 512;
+  int rpw = a.rpw;
+  if (rpw == 0) rpw = epi == EPI_QKV ? 2 : epi == EPI_SILU ? 2 : 1;
+#define MX_G1(KCH_, RPW_, EPI_, NORM_)                                                  \
+  if (kch == KCH_ && rpw == RPW_ && epi == EPI_ && norm == NORM_ && a.N % RPW_ == 0)     \
+    return launch_gemv1_t<KCH_, RPW_, EPI_, NORM_>(a, st);
+#define MX_G1K(KCH_)                                                                     \
+  MX_G1(KCH_, 2, EPI_QKV, true) MX_G1(KCH_, 1, EPI_RESID, false)                       \
+  MX_G1(KCH_, 2, EPI_RESID, false)                                                      \
+  MX_G1(KCH_, 2, EPI_SILU, true) MX_G1(KCH_, 4, EPI_SILU, true)                         \
+  MX_G1(KCH_, 1, EPI_STORE, false) MX_G1(KCH_, 1, EPI_STORE, true)
+  MX_G1K(1) MX_G1K(2) MX_G1K(4) MX_G1K(6) MX_G1K(8) MX_G1K(16)
+#undef MX_G1K
+#undef MX_G1
+  return hipErrorNotSupported;
+}
+
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
+  if (a.R == 1 && epi != EPI_ARGMAX && !a.force_legacy) {
+    const hipError_t e = launch_gemv1(a, epi, norm, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   // RT = 1 for the decode batch of 1; RT = 4 otherwise (prefill / batched decode).
   const int RT = a.R == 1 ? 1 : 4;
   const int ytiles = (a.R + RT - 1) / RT;
@@ -440,10 +804,21 @@ hipError_t gemv_prepare(int kmax) {
   return e;
 }
 
-hipError_t launch_attention(const AttnArgs& a, int R, hipStream_t st) {
-  hipLaunchKernelGGL(attn_partial_kernel, dim3(a.nsplit_max, a.kv_heads, R), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_combine_kernel, dim3(a.heads, R), dim3(128), 0, st, a);
-  return hipGetLastError();
+hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st) {
+  const int S = 128 * a.cpw;
+  const int nsplit = (max_len + S - 1) / S;
+  if (nsplit > ATT_MAX_SPLITS || (a.max_pos + S - 1) / S > a.split_stride || a.max_pos % 8)
+    return hipErrorInvalidValue;
+  const dim3 grid(nsplit, a.kv_heads, R);
+#define MX_AT(G_, C_)                                                              \
+  if (a.heads / a.kv_heads == G_ && a.cpw == C_) {                                 \
+    hipLaunchKernelGGL((attn_kernel<G_, C_>), grid, dim3(256), 0, st, a);          \
+    return hipGetLastError();                                                      \
+  }
+  MX_AT(1, 1) MX_AT(1, 2) MX_AT(1, 4) MX_AT(2, 1) MX_AT(2, 2) MX_AT(2, 4)
+  MX_AT(3, 1) MX_AT(3, 2) MX_AT(3, 4) MX_AT(4, 1) MX_AT(4, 2) MX_AT(4, 4)
+#undef MX_AT
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st) {

@@ -7,8 +7,10 @@ namespace mx {
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_QKV = 3, EPI_ARGMAX = 4 };
 
-constexpr int ATT_CHUNK = 64;  // positions per attention split
-constexpr int ATT_MAXG = 4;    // max q-heads per kv-head (one wave each)
+constexpr int ATT_S_MIN = 128;      // smallest split (positions) = 4 waves x 32
+constexpr int ATT_MAX_SPLITS = 256; // splits one launch may merge
+constexpr int ATT_MAXG = 4;         // max q-heads per kv-head
+constexpr int ATT_MERGE_CHUNK = 16; // splits whose partials the merging block prefetches
 
 struct GemvArgs {
   const uint16_t* W;       // [N][K] bf16, packed row order
@@ -21,6 +23,9 @@ struct GemvArgs {
   float* Y;                // STORE [R][N]; RESID [R][ystride] += ; SILU [R][N/2]
   int ystride;
   int max_blocks;          // grid cap (0 = default)
+  int force_legacy;        // 1: use the grid-stride kernel even for R = 1 (A/B timing)
+  int wpb;                 // R = 1 kernel: waves per block (4 or 8; 0 = 8)
+  int rpw;                 // R = 1 kernel: weight rows per wave (0 = default per epilogue)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -40,14 +45,18 @@ struct GemvArgs {
 struct AttnArgs {
   const float* Q;          // [R][heads][128]
   const uint16_t* kcache;  // this layer
-  const uint16_t* vcache;
+  const uint16_t* vcache;  // TRANSPOSED: [slot][kv_head][128][max_pos]
   const int32_t* row_slot;
   const int32_t* row_pos;
-  int heads, kv_heads, max_pos, nsplit_max;
+  int heads, kv_heads, max_pos;
+  int cpw;                 // 32-position chunks per wave: split = 128 * cpw positions
+  int split_stride;        // partial slots per (row, kv-head) >= max_pos / split
   float scale;
-  float* part_ml;          // [R][heads][nsplit_max][2]
-  float* part_acc;         // [R][heads][nsplit_max][128]
+  float* part_ml;          // [R][kv_heads][nsplit_max][grp][2]  (m, l) per split
+  float* part_acc;         // [R][kv_heads][nsplit_max][grp][128]
+  int* counter;            // [R][kv_heads] split arrival tickets (zero between launches)
   float* out;              // [R][heads*128]
+  int debug;               // timing experiments only (0 in the product path)
 };
 
 struct CommitArgs {
@@ -61,6 +70,7 @@ struct CommitArgs {
   const uint16_t* embed;
   float* h;
   int hidden, vocab, max_pos, pos_advance;
+  int scratch_slot;          // rows bound to this slot are parked: no advance, no history
 };
 
 hipError_t gemv_prepare(int kmax);
@@ -68,7 +78,7 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);
-hipError_t launch_attention(const AttnArgs& a, int R, hipStream_t st);
+hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st);
 hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t* embed,
                              int hidden, int vocab, uint8_t* seen, float* h, hipStream_t st);

@@ -85,12 +85,26 @@ class LlmEngine:
         self._check(self.lib.mx_llm_decode(self.h, n_rows, penalty,
                                            C.c_void_p(stream.cuda_stream)))
 
-    def decode_profiled(self, n_rows: int, penalty: float, stream):
-        ms, n = C.c_double(0.0), C.c_int(0)
+    PROFILE_CLASSES = ("qkv", "attention", "o_proj", "gate_up", "down", "lm_head", "commit")
+
+    def decode_profiled(self, n_rows: int, penalty: float, stream) -> Dict[str, float]:
+        """One eager step with HIP events around every launch: ms per launch class
+        (summed over layers) on the engine's own stream."""
+        n = len(self.PROFILE_CLASSES)
+        ms = (C.c_double * n)()
         self._check(self.lib.mx_llm_decode_profiled(self.h, n_rows, penalty,
-                                                    C.c_void_p(stream.cuda_stream),
-                                                    C.byref(ms), C.byref(n)))
-        return ms.value, n.value
+                                                    C.c_void_p(stream.cuda_stream), ms, n))
+        return {k: ms[i] for i, k in enumerate(self.PROFILE_CLASSES)}
+
+    def bench_attention(self, L: int, n_rows: int = 1, cpw: int = 1, debug: int = 0,
+                        reps: int = 200) -> float:
+        us = C.c_float(0.0)
+        self._check(self.lib.mx_llm_bench_attention(self.h, L, n_rows, cpw, debug, reps,
+                                                    C.byref(us)))
+        return us.value
+
+    def set_option(self, key: str, value: int) -> None:
+        self._check(self.lib.mx_llm_set_option(self.h, key.encode(), int(value)))
 
     def enable_logits(self) -> None:
         """Parity/debug mode: keep the penalised logits of each row (before first decode)."""

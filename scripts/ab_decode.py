@@ -1,0 +1,70 @@
+"""A/B decode-step variants on the full Orpheus-3B shape (synthetic weights), one process,
+interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+
+    python scripts/ab_decode.py [--pos 1200] [--reps 50] [--rounds 3]
+
+Each variant is a dict of mx_llm_set_option knobs; prints the hipGraph replay time of one
+B=1 step at position --pos for every round, and the median."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0,
+            "rpw_down": 0}
+VARIANTS = {
+    "base": {},
+    "att_cpw2": {"att_cpw": 2},
+    "att_cpw4": {"att_cpw": 4},
+    "rpw_gu4": {"rpw_gu": 4},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pos", type=int, default=1200)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    args = ap.parse_args()
+    import torch
+    from project_morpheus_amd import config as C
+    from project_morpheus_amd.engine import LlmEngine
+    from project_morpheus_amd.weights import synthetic_llm_weights
+    cfg = C.OrpheusConfig()
+    w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
+    llm = LlmEngine(cfg, w, device=0, max_slots=1, max_pos=2048, max_batch=1, max_prefill=256)
+    del w
+    torch.cuda.empty_cache()
+    st = torch.cuda.Stream()
+    prompt = list(range(1000, 1020))
+    names = args.variants.split(",")
+    res = {n: [] for n in names}
+    for rnd in range(args.rounds):
+        for name in names:
+            opts = dict(DEFAULTS, **VARIANTS[name])
+            for k, v in opts.items():
+                llm.set_option(k, v)
+            llm.prefill(0, 0, prompt, 1.1, st)
+            for _ in range(args.pos - len(prompt)):
+                llm.decode(1, 1.1, st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.reps):
+                llm.decode(1, 1.1, st)
+            e1.record(st)
+            e1.synchronize()
+            res[name].append(round(e0.elapsed_time(e1) / args.reps, 4))
+            llm.release_row(0, st)
+            st.synchronize()
+        print(f"round {rnd}: " + json.dumps({n: res[n][-1] for n in names}), flush=True)
+    print(json.dumps({n: {"median_ms": statistics.median(v), "all": v} for n, v in res.items()},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
