@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--max-tokens", type=int, default=MAX_TOKENS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", type=int, default=24)
+    p.add_argument("--step-pos", type=int, default=600,
+                   help="position at which the bare decode-step time is measured")
     return p.parse_args()
 
 
@@ -153,9 +155,17 @@ def main():
         dist.all_gather_object(fl, firsts)
         firsts = [x for r in fl for x in r]
 
-    # ---- roofline of the dominant kernel (gate/up GEMV: 2*ffn*hidden bf16 per launch) ----
-    # eager steps with HIP events on the engine's own stream around every launch
+    # ---- roofline of the dominant kernel (gate/up GEMV, 2*ffn*hidden bf16 per launch) ----
+    # HIP events around one hipGraph of back-to-back launches of that kernel sweeping all 28
+    # layers' weights (as a decode step streams them), on the engine's capture stream
     st = syn.stream
+    st.synchronize()
+    gemv_us = {}
+    for kind in ("gate_up", "qkv", "o_proj", "down"):
+        us, nbytes = llm.bench_gemv(kind, reps=4)
+        gemv_us[kind] = (us, nbytes)
+    gu_us, gu_bytes = gemv_us["gate_up"]
+    gu_gbs = gu_bytes / (gu_us * 1e-6) / 1e9
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(3):
         llm.decode(1, 1.1, st)
@@ -164,19 +174,21 @@ def main():
         for k, v in llm.decode_profiled(1, 1.1, st).items():
             prof[k] = prof.get(k, 0.0) + v
     per_step_us = {k: round(1e3 * v / args.profile_steps, 2) for k, v in prof.items()}
-    gu_ms = prof["gate_up"] / (args.profile_steps * cfg.layers)
-    gu_bytes = 2 * cfg.ffn * cfg.hidden * 2
-    gu_gbs = gu_bytes / (gu_ms * 1e-3) / 1e9
+    llm.release_row(0, st)
+    st.synchronize()
     # pure decode step (graph replay, no SNAC) against the whole-step byte roofline
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n_rep = 50
+    llm.prefill(0, 0, prompt, 1.1, st)
+    for _ in range(args.step_pos - len(prompt)):   # measure the step at a mid-utterance length
+        llm.decode(1, 1.1, st)
     ev0.record(st)
     for _ in range(n_rep):
         llm.decode(1, 1.1, st)
     ev1.record(st)
     ev1.synchronize()
     step_ms = ev0.elapsed_time(ev1) / n_rep
-    pos = len(prompt) + 3 + args.profile_steps + n_rep
+    pos = args.step_pos + n_rep // 2
     step_bytes = cfg.step_weight_bytes() + pos * cfg.kv_bytes_per_position()
     llm.release_row(0, st)
     st.synchronize()
@@ -201,12 +213,14 @@ def main():
             "decode_tok_per_s": round(1e3 / step_ms, 1),
             "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),
                               "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4)},
-            "roofline": {"kernel": "gemv_kernel<1,2,EPI_SILU,NORM> (gate/up + SiLU*up)",
+            "roofline": {"kernel": "gemv1_kernel<6,2,EPI_SILU,NORM,4> (RMSNorm + gate/up + SiLU*up)",
                          "bound": "hbm", "achieved": round(gu_gbs, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
-                         "avg_launch_us": round(gu_ms * 1e3, 3), "bytes_per_launch": gu_bytes,
+                         "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
                          "traffic": None},
             "eager_step_us_by_kernel": per_step_us,
+            "gemv_graph_us": {k: {"us": round(v[0], 2), "GB/s": round(v[1] / v[0] / 1e3, 1)}
+                              for k, v in gemv_us.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, prompt)

@@ -653,6 +653,75 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
   return MX_OK;
 }
 
+// Roofline probe: one hipGraph of `reps` sweeps over all layers' GEMV `which` (0 qkv,
+// 1 o-proj, 2 gate/up, 3 down) for a single row, exactly as the decode step launches them
+// (same kernels, grids and epilogues; decode row 0's state is used and clobbered: the
+// residual / KV scratch written are meaningless).  Sweeping every layer keeps the stream
+// out of the 256 MB Infinity Cache, as in a real step.  Writes mean microseconds per
+// launch (inter-kernel gap in the graph included) and the weight bytes of one launch.
+extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int reps, float* us_out,
+                                 double* bytes_out) {
+  if (!x || !us_out || which < 0 || which > 3 || reps < 1) return MX_ERR_ARG;
+  if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
+  const auto& c = x->c;
+  const int H = c.hidden, QD = c.heads * 128;
+  MX_TRY(x, hipSetDevice(x->device));
+  hipStream_t st = x->cap;
+  auto args = [&](int li) {
+    const LayerW& l = x->L[li];
+    GemvArgs g{};
+    g.R = 1; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
+    if (which == 0) {
+      g.W = l.wqkv; g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
+      g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = x->row_slot;
+      g.row_pos = x->row_pos; g.kcache = x->kcache + x->kv_layer_elems * li;
+      g.vcache = x->vcache + x->kv_layer_elems * li; g.heads = c.heads; g.kv_heads = c.kv_heads;
+      g.max_pos = c.max_pos; g.Q = x->q;
+    } else if (which == 1) {
+      g.W = l.wo; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act; g.rpw = x->rpw_o;
+    } else if (which == 2) {
+      g.W = l.wgu; g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
+      g.rpw = x->rpw_gu;
+    } else {
+      g.W = l.wd; g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
+    }
+    g.xstride = g.K; g.ystride = g.N;
+    return g;
+  };
+  const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : EPI_RESID;
+  const bool norm = which == 0 || which == 2;
+  MX_TRY(x, launch_gemv(args(0), epi, norm, st));
+  MX_TRY(x, hipStreamSynchronize(st));
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  MX_TRY(x, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < reps && e == hipSuccess; ++i)
+    for (int li = 0; li < c.layers && e == hipSuccess; ++li) e = launch_gemv(args(li), epi, norm, st);
+  hipError_t e2 = hipStreamEndCapture(st, &g);
+  MX_TRY(x, e);
+  MX_TRY(x, e2);
+  MX_TRY(x, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  hipEvent_t e0, e1;
+  MX_TRY(x, hipEventCreate(&e0));
+  MX_TRY(x, hipEventCreate(&e1));
+  MX_TRY(x, hipGraphLaunch(ge, st));
+  MX_TRY(x, hipEventRecord(e0, st));
+  MX_TRY(x, hipGraphLaunch(ge, st));
+  MX_TRY(x, hipEventRecord(e1, st));
+  MX_TRY(x, hipEventSynchronize(e1));
+  float ms = 0.f;
+  MX_TRY(x, hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipGraphExecDestroy(ge);
+  (void)hipGraphDestroy(g);
+  *us_out = 1e3f * ms / (reps * c.layers);
+  const GemvArgs a0 = args(0);
+  if (bytes_out) *bytes_out = 2.0 * a0.N * a0.K;
+  return MX_OK;
+}
+
 extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   if (!x || !key) return MX_ERR_ARG;
   const std::string k(key);
@@ -741,7 +810,7 @@ struct mx_snac {
   std::vector<void*> allocs;
   float* up_packed[4][8] = {};  // per block, per phase: [Cout][2*Cin]
   int up_delta[4][8][2] = {};
-  float *bufA = nullptr, *bufB = nullptr, *noise = nullptr;
+  float *bufA = nullptr, *bufB = nullptr, *bufC = nullptr, *noise = nullptr;
   size_t buf_elems = 0;
   bool final = false;
 };
@@ -795,7 +864,8 @@ extern "C" int mx_snac_create(int device, int max_frames, int max_batch, mx_snac
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, s->buf_elems * 4);
   if (e == hipSuccess) { s->allocs.push_back(p); s->bufA = (float*)p; e = hipMalloc(&p, s->buf_elems * 4); }
-  if (e == hipSuccess) { s->allocs.push_back(p); s->bufB = (float*)p; e = hipMalloc(&p, (size_t)3360 * max_frames * max_batch * 4); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->bufB = (float*)p; e = hipMalloc(&p, s->buf_elems * 4); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->bufC = (float*)p; e = hipMalloc(&p, (size_t)3360 * max_frames * max_batch * 4); }
   if (e == hipSuccess) { s->allocs.push_back(p); s->noise = (float*)p; }
   if (e != hipSuccess) {
     g_err = std::string("snac alloc failed: ") + hipGetErrorString(e);
@@ -867,6 +937,18 @@ extern "C" int mx_snac_finalize(mx_snac* s) {
   return MX_OK;
 }
 
+// Tile choice for one conv-GEMM: 64-wide column tiles on long sequences, and as many
+// K-splitting waves per tile as keep the launch near 2k waves (early stages have few
+// output columns and long K, late stages the opposite).
+static void pick_tiles(ConvGemmArgs& g, int nphase) {
+  g.nsub = g.Tin >= 2048 ? 4 : 2;
+  const int tiles = (g.M / 32) * ((g.Tin + 16 * g.nsub - 1) / (16 * g.nsub)) * nphase * g.B;
+  const int Ktot = g.nseg * g.Cin;
+  g.wk = 1;
+  while (g.wk < 8 && tiles * g.wk * 2 <= 2048 && Ktot % (32 * g.wk) == 0 && Ktot / (2 * g.wk) >= 64)
+    g.wk *= 2;
+}
+
 extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, int batch,
                               const float* noise, uint64_t seed, int16_t* pcm, float* audio,
                               int lo, int hi, void* stream) {
@@ -883,8 +965,9 @@ extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, i
   auto W = [&](const std::string& n) { return s->w[n]; };
   const int B = batch;
   int T = 4 * n_frames;
-  float* x = s->bufA;
-  float* y = s->bufB;
+  float* A = s->bufA;  // block activations x
+  float* Bf = s->bufB; // scratch (dwconv output, ConvTranspose output)
+  float* Cs = s->bufC; // Snake(x) for the next ConvTranspose / output conv
   // noise layout per window: [32N | 256N | 1024N | 2048N]
   const int nlen = 3360 * n_frames;
   const float* nz = noise;
@@ -895,48 +978,60 @@ extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, i
   const float* cb[3] = {W("q0.codebook"), W("q1.codebook"), W("q2.codebook")};
   const float* pw[3] = {W("q0.out_proj.w"), W("q1.out_proj.w"), W("q2.out_proj.w")};
   const float* pb[3] = {W("q0.out_proj.b"), W("q1.out_proj.b"), W("q2.out_proj.b")};
-  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, x, st));        // x: [768][T]
-  MX_TRY(s, launch_dwconv(x, y, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
+  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, A, st));        // A: [768][T]
+  MX_TRY(s, launch_dwconv(A, Bf, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
   {
     ConvGemmArgs g{};
-    g.A = W("in.pw.w"); g.X = y; g.bias = W("in.pw.b"); g.out = x; g.M = 1024; g.Cin = 768;
-    g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_STORE;
-    MX_TRY(s, launch_conv_gemm(g, B, st));                                      // x: [1024][T]
+    g.Aph[0] = W("in.pw.w"); g.X = Bf; g.bias = W("in.pw.b"); g.out = A; g.M = 1024; g.Cin = 768;
+    g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1; g.col_stride = 1; g.epi = CG_STORE;
+    g.out2 = Cs; g.alpha2 = W("b0.alpha");
+    pick_tiles(g, 1);
+    MX_TRY(s, launch_conv_gemm(g, 1, st));                                      // A: [1024][T]
   }
   int noff = 0;
   for (int b = 0; b < 4; ++b) {
     const int cin = 1024 >> b, cout = cin / 2, sr = kRates[b];
     const std::string p = "b" + std::to_string(b) + ".";
     const int To = T * sr;
-    for (int ph = 0; ph < sr; ++ph) {  // Snake + ConvTranspose1d: x [cin][T] -> y [cout][To]
+    {  // ConvTranspose1d on Snake(x): all sr phases in one launch, Cs [cin][T] -> Bf [cout][To]
       ConvGemmArgs g{};
-      g.A = s->up_packed[b][ph]; g.X = x; g.alpha = W(p + "alpha"); g.bias = W(p + "up.b");
-      g.out = y; g.M = cout; g.Cin = cin; g.Tin = T; g.Tout = To; g.nseg = 2;
-      g.delta[0] = s->up_delta[b][ph][0]; g.delta[1] = s->up_delta[b][ph][1];
-      g.col_stride = sr; g.col_off = ph; g.epi = CG_STORE;
-      MX_TRY(s, launch_conv_gemm(g, B, st));
+      for (int ph = 0; ph < sr; ++ph) {
+        g.Aph[ph] = s->up_packed[b][ph];
+        g.dph[ph][0] = s->up_delta[b][ph][0];
+        g.dph[ph][1] = s->up_delta[b][ph][1];
+      }
+      g.X = Cs; g.bias = W(p + "up.b"); g.out = Bf; g.M = cout; g.Cin = cin; g.Tin = T;
+      g.Tout = To; g.B = B; g.nseg = 2; g.col_stride = sr; g.epi = CG_STORE;
+      pick_tiles(g, sr);
+      MX_TRY(s, launch_conv_gemm(g, sr, st));
     }
     T = To;
-    {  // NoiseBlock: x = y + noise * (Wn y)
+    {  // NoiseBlock: A = Bf + noise * (Wn Bf)
       ConvGemmArgs g{};
-      g.A = W(p + "noise.w"); g.X = y; g.R = y; g.noise = nz + noff; g.noise_stride = nlen;
-      g.out = x; g.M = cout;
-      g.Cin = cout; g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_NOISE;
-      MX_TRY(s, launch_conv_gemm(g, B, st));
+      g.Aph[0] = W(p + "noise.w"); g.X = Bf; g.R = Bf; g.noise = nz + noff; g.noise_stride = nlen;
+      g.out = A; g.M = cout; g.Cin = cout; g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1;
+      g.col_stride = 1; g.epi = CG_NOISE;
+      pick_tiles(g, 1);
+      MX_TRY(s, launch_conv_gemm(g, 1, st));
     }
     noff += T;
-    for (int r = 0; r < 3; ++r) {  // ResidualUnit(d): x += pw(Snake(dw_d(Snake(x))))
+    for (int r = 0; r < 3; ++r) {  // ResidualUnit(d): A += pw(Snake(dw_d(Snake(A))))
       const std::string q = p + "r" + std::to_string(r) + ".";
-      MX_TRY(s, launch_dwconv(x, y, W(q + "dw.w"), W(q + "dw.b"), W(q + "alpha1"),
+      MX_TRY(s, launch_dwconv(A, Bf, W(q + "dw.w"), W(q + "dw.b"), W(q + "alpha1"),
                               W(q + "alpha2"), B, cout, T, kDil[r], st));
       ConvGemmArgs g{};
-      g.A = W(q + "pw.w"); g.X = y; g.bias = W(q + "pw.b"); g.R = x; g.out = x; g.M = cout;
-      g.Cin = cout; g.Tin = T; g.Tout = T; g.nseg = 1; g.col_stride = 1; g.epi = CG_RESID;
-      MX_TRY(s, launch_conv_gemm(g, B, st));
+      g.Aph[0] = W(q + "pw.w"); g.X = Bf; g.bias = W(q + "pw.b"); g.R = A; g.out = A;
+      g.M = cout; g.Cin = cout; g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1; g.col_stride = 1;
+      g.epi = CG_RESID;
+      if (r == 2) {  // the block's output feeds Snake -> next ConvTranspose / output conv
+        g.out2 = Cs;
+        g.alpha2 = b < 3 ? W("b" + std::to_string(b + 1) + ".alpha") : W("out.alpha");
+      }
+      pick_tiles(g, 1);
+      MX_TRY(s, launch_conv_gemm(g, 1, st));
     }
   }
-  MX_TRY(s, launch_snac_out(x, W("out.alpha"), W("out.conv.w"), W("out.conv.b"), B, T, lo, hi,
-                            audio, pcm, st));
+  MX_TRY(s, launch_snac_out(Cs, W("out.conv.w"), W("out.conv.b"), B, T, lo, hi, audio, pcm, st));
   return MX_OK;
 }
 

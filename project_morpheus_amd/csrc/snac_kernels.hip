@@ -101,119 +101,221 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, c
 }
 
 // ---------------------------------------------------------------------------------
-// Segmented conv-GEMM on f32 MFMA 16x16x4.
-//   out[b][m][col_stride*n + col_off] = epi( sum_seg sum_ci A[m][seg*Cin+ci]
-//                                            * f(X[b][ci][n + delta_seg]) )
-// Tile 64 (M) x 64 (n) x 16 (k); 4 waves, each a 32x32 sub-tile of 2x2 MFMA tiles.
-// Grid (ceil(Tin/64), M/64, B).
+// Segmented conv-GEMM on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32), operands straight
+// from global memory (weights are read once per column tile, activations are L2-resident).
+//   out[b][m][col_stride*n + ph] = epi( sum_seg sum_ci A_ph[m][seg*Cin+ci] X[b][ci][n+d_ph,seg] )
+// One block = one 32 x (16*NSUB) output tile of one (phase, window); its WK waves split K
+// and their partial tiles are summed in LDS in a fixed order (deterministic, no atomics).
+// MFMA j of a 16-deep k chunk contracts k = kc + 4g + j over the lane groups g, so every
+// lane fetches its A operand as one float4 (4 consecutive k of one row).
+// Grid (ceil(Tin / (16*NSUB)), M / 32, nphase * B).
 // ---------------------------------------------------------------------------------
-constexpr int CG_BM = 64, CG_BN = 64, CG_BK = 16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGemmArgs a) {
-  __shared__ float As[CG_BK][CG_BM + 4];
-  __shared__ float Bs[CG_BK][CG_BN + 4];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int n0 = blockIdx.x * CG_BN, m0 = blockIdx.y * CG_BM, bt = blockIdx.z;
+template <int WK, int NSUB>
+__global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
+  constexpr int BM = 32, BN = 16 * NSUB;
+  const int lane = threadIdx.x & 63, wk = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int ph = blockIdx.z / a.B, bt = blockIdx.z - ph * a.B;
+  const float* A = a.Aph[ph];
+  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
   const int Ktot = a.nseg * a.Cin;
+  const int Kw = Ktot / WK;
   const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
-  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
-  floatx4 acc[2][2];
+
+  f32x4 acc[2][NSUB];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NSUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // loader mapping: A: thread -> (row m = tid/4, k quad = (tid%4)*4); B: (k = tid/16, n quad)
-  const int am = tid >> 2, ak = (tid & 3) * 4;
-  const int bk = tid >> 4, bn = (tid & 15) * 4;
-  for (int k0 = 0; k0 < Ktot; k0 += CG_BK) {
-    {
-      const float4 v = *reinterpret_cast<const float4*>(a.A + (size_t)(m0 + am) * Ktot + k0 + ak);
-      As[ak + 0][am] = v.x;
-      As[ak + 1][am] = v.y;
-      As[ak + 2][am] = v.z;
-      As[ak + 3][am] = v.w;
-    }
-    {
-      const int kk = k0 + bk;
-      const int seg = kk / a.Cin, ci = kk - seg * a.Cin;
-      const int d = seg == 0 ? a.delta[0] : a.delta[1];
-      const float* xr = X + (size_t)ci * a.Tin;
-      const float al = a.alpha ? a.alpha[ci] : 0.f;
+  // this lane's output columns (B operand) and their validity
+  int tn[NSUB];
+  bool nok[NSUB];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int t = n0 + bn + q + d;
-        float v = 0.f;
-        if (n0 + bn + q < a.Tin && t >= 0 && t < a.Tin) {
-          v = xr[t];
-          if (a.alpha) v = snake(v, al);
-        }
-        Bs[bk][bn + q] = v;
+  for (int j = 0; j < NSUB; ++j) {
+    tn[j] = n0 + 16 * j + c;
+    nok[j] = tn[j] < a.Tin;
+  }
+  const float* Ar0 = A + (size_t)(m0 + c) * Ktot;
+  const float* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot;
+  for (int kc = wk * Kw; kc < (wk + 1) * Kw; kc += 16) {
+    const int k4 = kc + 4 * g;
+    const float4 a0 = *reinterpret_cast<const float4*>(Ar0 + k4);
+    const float4 a1 = *reinterpret_cast<const float4*>(Ar1 + k4);
+    const int seg = kc >= a.Cin ? 1 : 0;  // a 16-chunk never straddles segments
+    const int ci0 = k4 - seg * a.Cin;
+    const int d = seg ? d1 : d0;
+    float bv[NSUB][4];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int t = tn[j] + d;
+      const bool ok = nok[j] && t >= 0 && t < a.Tin;
+      const int tc = min(max(t, 0), a.Tin - 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
+        bv[j][e] = ok ? v : 0.f;
       }
     }
-    __syncthreads();
+    const float av0[4] = {a0.x, a0.y, a0.z, a0.w};
+    const float av1[4] = {a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-    for (int k4 = 0; k4 < CG_BK; k4 += 4) {
-      const int kr = k4 + (lane >> 4);
-      const float a0 = As[kr][wm + (lane & 15)];
-      const float a1 = As[kr][wm + 16 + (lane & 15)];
-      const float b0 = Bs[kr][wn + (lane & 15)];
-      const float b1 = Bs[kr][wn + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) {
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv[j][e], acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv[j][e], acc[1][j], 0, 0, 0);
+      }
     }
+  }
+
+  // deterministic cross-wave K reduction through LDS: tile [BM][BN] per wave
+  __shared__ float red[WK][BM * BN];
+  if (WK > 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+          red[wk][(16 * i + 4 * g + rg) * BN + 16 * j + c] = acc[i][j][rg];
     __syncthreads();
   }
-  // epilogue: C/D map for 16x16: col = lane & 15, row = (lane >> 4) * 4 + reg
+  // epilogue: thread -> tile elements
+  for (int e = threadIdx.x; e < BM * BN; e += WK * 64) {
+    const int mm = e / BN, nn = e - mm * BN;
+    const int n = n0 + nn;
+    if (n >= a.Tin) continue;
+    float v;
+    if (WK > 1) {
+      v = red[0][e];
+#pragma unroll
+      for (int w = 1; w < WK; ++w) v += red[w][e];
+    } else {
+      // WK == 1: the wave's own registers hold the tile; route through LDS anyway
+      v = 0.f;
+    }
+    const int m = m0 + mm;
+    const int col = a.col_stride * n + ph;
+    if (a.bias) v += a.bias[m];
+    const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
+    if (a.epi == CG_RESID) v = a.R[o] + v;
+    else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
+    a.out[o] = v;
+    if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
+  }
+}
+
+// WK == 1 specialisation of the epilogue path: write straight from registers.
+template <int NSUB>
+__global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
+  constexpr int BM = 32, BN = 16 * NSUB;
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int ph = blockIdx.z / a.B, bt = blockIdx.z - ph * a.B;
+  const float* A = a.Aph[ph];
+  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
+  const int Ktot = a.nseg * a.Cin;
+  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
+  f32x4 acc[2][NSUB];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NSUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tn[NSUB];
+  bool nok[NSUB];
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + reg;
-        const int n = n0 + wn + j * 16 + (lane & 15);
-        if (n >= a.Tin) continue;
-        const int col = a.col_stride * n + a.col_off;
-        float v = acc[i][j][reg];
+  for (int j = 0; j < NSUB; ++j) {
+    tn[j] = n0 + 16 * j + c;
+    nok[j] = tn[j] < a.Tin;
+  }
+  const float* Ar0 = A + (size_t)(m0 + c) * Ktot;
+  const float* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot;
+  for (int kc = 0; kc < Ktot; kc += 16) {
+    const int k4 = kc + 4 * g;
+    const float4 a0 = *reinterpret_cast<const float4*>(Ar0 + k4);
+    const float4 a1 = *reinterpret_cast<const float4*>(Ar1 + k4);
+    const int seg = kc >= a.Cin ? 1 : 0;
+    const int ci0 = k4 - seg * a.Cin;
+    const int d = seg ? d1 : d0;
+    float bv[NSUB][4];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int t = tn[j] + d;
+      const bool ok = nok[j] && t >= 0 && t < a.Tin;
+      const int tc = min(max(t, 0), a.Tin - 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
+        bv[j][e] = ok ? v : 0.f;
+      }
+    }
+    const float av0[4] = {a0.x, a0.y, a0.z, a0.w};
+    const float av1[4] = {a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) {
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv[j][e], acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv[j][e], acc[1][j], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int n = n0 + 16 * j + c;
+      if (n >= a.Tin) continue;
+      const int col = a.col_stride * n + ph;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int m = m0 + 16 * i + 4 * g + rg;
+        float v = acc[i][j][rg];
         if (a.bias) v += a.bias[m];
         const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
         if (a.epi == CG_RESID) v = a.R[o] + v;
         else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
         a.out[o] = v;
+        if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
       }
+    }
 }
 
 // ---------------------------------------------------------------------------------
-// Output stage: Snake(64) -> conv 64->1 k7 pad 3 (+bias) -> tanh; PCM16 epilogue on the
+// Output stage: conv 64->1 k7 pad 3 (+bias) -> tanh on the Snake-activated input (the
+// last ResidualUnit's epilogue wrote Snake(x, out.alpha)), then the PCM16 epilogue on the
 // [lo, hi) slice: (x * 32767) truncated toward zero, as (audio_slice*32767).to(int16).
-// Grid (ceil(T/256), B), block 256.
+// Grid (ceil(T/64), B), block 256: 4 lanes per output sample split the 64 channels.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void snac_out_kernel(const float* x, const float* alpha,
-                                                       const float* w, const float* b, int T,
-                                                       int lo, int hi, float* audio,
-                                                       int16_t* pcm) {
+__global__ __launch_bounds__(256) void snac_out_kernel(const float* xs, const float* w,
+                                                       const float* b, int T, int lo, int hi,
+                                                       float* audio, int16_t* pcm) {
   const int bt = blockIdx.y;
-  const int t0 = blockIdx.x * 256;
-  __shared__ float tile[64][256 + 6];
-  const float* xb = x + (size_t)bt * 64 * T;
-  for (int i = threadIdx.x; i < 64 * 262; i += 256) {
-    const int c = i / 262, j = i - c * 262;
-    const int t = t0 - 3 + j;
-    float v = 0.f;
-    if (t >= 0 && t < T) v = snake(xb[(size_t)c * T + t], alpha[c]);
-    tile[c][j] = v;
-  }
-  __syncthreads();
-  const int t = t0 + threadIdx.x;
-  if (t >= T) return;
-  float acc = b[0];
-  for (int c = 0; c < 64; ++c)
+  const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int part = threadIdx.x & 3;  // channels part*16 .. part*16+15
+  const float* xb = xs + (size_t)bt * 64 * T;
+  float acc = 0.f;
+  if (t < T) {
+    for (int cc = 0; cc < 16; ++cc) {
+      const int ch = part * 16 + cc;
+      const float* xr = xb + (size_t)ch * T;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) acc = fmaf(w[c * 7 + k], tile[c][threadIdx.x + k], acc);
-  const float v = tanhf(acc);
+      for (int k = 0; k < 7; ++k) {
+        const int tt = t + k - 3;
+        const float v = (tt >= 0 && tt < T) ? xr[tt] : 0.f;
+        acc = fmaf(w[ch * 7 + k], v, acc);
+      }
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  if (t >= T || part != 0) return;
+  const float v = tanhf(acc + b[0]);
   if (audio) audio[(size_t)bt * T + t] = v;
   if (pcm && t >= lo && t < hi) {
     const float s = v * 32767.0f;
@@ -262,18 +364,29 @@ hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* 
   return hipGetLastError();
 }
 
-hipError_t launch_conv_gemm(const ConvGemmArgs& a, int B, hipStream_t st) {
-  if (a.M % CG_BM || (a.nseg * a.Cin) % CG_BK || a.Cin % CG_BK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_gemm_kernel, dim3((a.Tin + CG_BN - 1) / CG_BN, a.M / CG_BM, B),
-                     dim3(256), 0, st, a);
-  return hipGetLastError();
+hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
+  const int Ktot = a.nseg * a.Cin;
+  if (a.M % 32 || a.Cin % 16 || Ktot % (16 * a.wk)) return hipErrorInvalidValue;
+  const int bn = 16 * a.nsub;
+  const dim3 grid((a.Tin + bn - 1) / bn, a.M / 32, nphase * a.B);
+#define MX_CG(WK_, NS_)                                                                   \
+  if (a.wk == WK_ && a.nsub == NS_) {                                                     \
+    if (WK_ == 1)                                                                         \
+      hipLaunchKernelGGL((conv_gemm1_kernel<NS_>), grid, dim3(64), 0, st, a);             \
+    else                                                                                  \
+      hipLaunchKernelGGL((conv_gemm_kernel<WK_, NS_>), grid, dim3(WK_ * 64), 0, st, a);   \
+    return hipGetLastError();                                                             \
+  }
+  MX_CG(1, 2) MX_CG(1, 4) MX_CG(2, 2) MX_CG(2, 4) MX_CG(4, 2) MX_CG(4, 4) MX_CG(8, 2)
+  MX_CG(8, 4)
+#undef MX_CG
+  return hipErrorInvalidValue;
 }
 
-hipError_t launch_snac_out(const float* x, const float* alpha, const float* w, const float* b,
-                           int B, int T, int lo, int hi, float* audio, int16_t* pcm,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(snac_out_kernel, dim3((T + 255) / 256, B), dim3(256), 0, st, x, alpha, w,
-                     b, T, lo, hi, audio, pcm);
+hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
+                           int lo, int hi, float* audio, int16_t* pcm, hipStream_t st) {
+  hipLaunchKernelGGL(snac_out_kernel, dim3((T + 63) / 64, B), dim3(256), 0, st, xs, w, b, T, lo,
+                     hi, audio, pcm);
   return hipGetLastError();
 }
 

@@ -96,6 +96,16 @@ class LlmEngine:
                                                     C.c_void_p(stream.cuda_stream), ms, n))
         return {k: ms[i] for i, k in enumerate(self.PROFILE_CLASSES)}
 
+    GEMV_KINDS = {"qkv": 0, "o_proj": 1, "gate_up": 2, "down": 3}
+
+    def bench_gemv(self, which: str, reps: int = 4):
+        """(mean µs per launch, weight bytes per launch) of a single-row GEMV, timed in a
+        hipGraph sweeping all layers (roofline probe; idle context only)."""
+        us, nb = C.c_float(0.0), C.c_double(0.0)
+        self._check(self.lib.mx_llm_bench_gemv(self.h, self.GEMV_KINDS[which], reps,
+                                               C.byref(us), C.byref(nb)))
+        return us.value, nb.value
+
     def bench_attention(self, L: int, n_rows: int = 1, cpw: int = 1, debug: int = 0,
                         reps: int = 200) -> float:
         us = C.c_float(0.0)
