@@ -762,6 +762,10 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported) return e;
   }
+  if (a.R >= 2 && !a.force_legacy) {
+    const hipError_t e = launch_gemm_rows(a, epi, norm, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   // RT = 1 for the decode batch of 1; RT = 4 otherwise (prefill / batched decode).
   const int RT = a.R == 1 ? 1 : 4;
   const int ytiles = (a.R + RT - 1) / RT;

@@ -75,6 +75,8 @@ struct CommitArgs {
 
 hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
+// R >= 2 rows on bf16 MFMA (llm_batched.hip); hipErrorNotSupported if the shape is not covered
+hipError_t launch_gemm_rows(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);

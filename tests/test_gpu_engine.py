@@ -52,7 +52,7 @@ def test_utterance_matches_oracle(setup):
     for k, (g, r) in enumerate(zip(st.token_ids, r_toks)):
         if g != r:
             top2 = np.sort(r_logits[k].numpy())[-2:]
-            assert top2[1] - top2[0] < 1e-3, f"step {k}"
+            assert top2[1] - top2[0] < 1e-2, f"step {k}"  # bf16-KV near-tie (test_gpu_llm.py)
             break
     # audio: same schedule + same windows through the CPU SNAC oracle
     strings = [f"<custom_token_{t - C.CUSTOM_TOKEN_BASE}>" for t in inject]

@@ -1,8 +1,12 @@
 """GPU parity of the decode step (HIP kernels via the C ABI) vs the fp32 CPU oracle.
 
 Tolerances (precision contract): per-step penalised logits within
-atol 2e-3 + rtol 2e-3 of the oracle; greedy tokens identical, tie-aware: a divergence is
-accepted only where the oracle's top-2 margin is below 1e-3 (then the comparison stops).
+atol 5e-3 + rtol 5e-3 of the oracle; greedy tokens identical, tie-aware: a token may differ
+from the oracle's argmax only where the oracle's top-2 margin is below 1e-2 (the harness is
+teacher-forced, so later steps are still compared).  Why 5e-3: K and V are rounded to bf16
+in the cache (as vLLM's bf16 cache does), so a last-ulp fp32 difference in k or v can flip a
+bf16 rounding; measured (scripts/parity_probe.py) the max logit difference is 2.1e-3 for the
+exact-fp32 VALU path and the MFMA path alike, against 2.6e-2 for an oracle with fp32 KV.
 """
 import numpy as np
 import pytest
@@ -13,6 +17,9 @@ from project_morpheus_amd import config as C
 from project_morpheus_amd.weights import synthetic_llm_weights
 
 pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 5e-3   # see module docstring
+TIE_MARGIN = 1e-2
 
 
 def _cfgs(kind):
@@ -48,7 +55,7 @@ def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512):
 def _compare(cfg, w, prompt, steps, penalty=1.1):
     """Teacher-forced comparison: the oracle is fed the GPU's tokens, so every step's
     logits are compared; a token may differ from the oracle's own argmax only where the
-    oracle's top-2 margin is below 1e-3 (near-tie).  Returns the number of steps whose
+    oracle's top-2 margin is below TIE_MARGIN (near-tie).  Returns the number of steps whose
     argmax agreed."""
     g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, penalty)
     ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=512)
@@ -57,12 +64,12 @@ def _compare(cfg, w, prompt, steps, penalty=1.1):
     agree = 0
     for k in range(steps):
         rl = r_logits[k].numpy()
-        np.testing.assert_allclose(g_logits[k], rl, atol=2e-3, rtol=2e-3,
+        np.testing.assert_allclose(g_logits[k], rl, atol=LOGIT_TOL, rtol=LOGIT_TOL,
                                    err_msg=f"logits step {k}")
         assert g_toks[k] == int(np.argmax(g_logits[k]))
         if g_toks[k] != int(np.argmax(rl)):
             top2 = np.sort(rl)[-2:]
-            assert top2[1] - top2[0] < 1e-3, f"token mismatch at step {k} (margin {top2[1]-top2[0]})"
+            assert top2[1] - top2[0] < TIE_MARGIN, f"token mismatch at step {k} (margin {top2[1]-top2[0]})"
         else:
             agree += 1
     return agree
@@ -117,3 +124,69 @@ def test_bad_args_fail_loudly():
     bad.pop("l1.wd")
     with pytest.raises(_lib.MxError):
         LlmEngine(cfg, bad, max_slots=1, max_pos=128)   # incomplete weights
+
+
+def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None):
+    """Batched decode: every prompt on its own slot and decode row, all rows stepped together
+    (the B >= 2 MFMA path); each row teacher-forced against its own oracle run."""
+    from project_morpheus_amd.engine import LlmEngine
+    B = len(prompts)
+    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=512, max_batch=max_batch or B,
+                    max_prefill=256)
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    toks = [[] for _ in range(B)]
+    logits = [[] for _ in range(B)]
+    for r, p in enumerate(prompts):
+        eng.prefill(r, r, p, penalty, st)
+    for k in range(steps):
+        if k > 0:
+            eng.decode(B, penalty, st)
+        st.synchronize()
+        for r, p in enumerate(prompts):
+            logits[r].append(eng.read_logits(r, st))
+            toks[r].append(int(eng.hist[r, len(p) + k]))
+    eng.close()
+    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=512)
+    agree = 0
+    for r, p in enumerate(prompts):
+        _, r_logits = L.greedy_generate(ref, p, steps, penalty, return_logits=True,
+                                        forced=toks[r])
+        for k in range(steps):
+            rl = r_logits[k].numpy()
+            np.testing.assert_allclose(logits[r][k], rl, atol=LOGIT_TOL, rtol=LOGIT_TOL,
+                                       err_msg=f"row {r} step {k}")
+            assert toks[r][k] == int(np.argmax(logits[r][k]))
+            if toks[r][k] != int(np.argmax(rl)):
+                top2 = np.sort(rl)[-2:]
+                assert top2[1] - top2[0] < TIE_MARGIN, f"row {r} step {k}"
+            else:
+                agree += 1
+    return agree
+
+
+def test_batched_decode_20_rows_small():
+    """20 concurrent streams (32-row MFMA tiles), ragged prompt lengths 5..43."""
+    cfg = _cfgs("small")
+    w = synthetic_llm_weights(cfg, seed=31, std=0.05, norm_jitter=0.5)
+    rng = np.random.default_rng(7)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 5 + 2 * i)] for i in range(20)]
+    assert _compare_rows(cfg, w, prompts, 12) >= 0.8 * 20 * 12
+
+
+def test_batched_decode_40_rows_small():
+    """40 streams: 64-row tiles (the 4-subtile register layout)."""
+    cfg = _cfgs("small")
+    w = synthetic_llm_weights(cfg, seed=32, std=0.05, norm_jitter=0.5)
+    rng = np.random.default_rng(8)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 3 + i)] for i in range(40)]
+    assert _compare_rows(cfg, w, prompts, 6) >= 0.8 * 40 * 6
+
+
+def test_batched_decode_orpheus_width_4_rows():
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=1)
+    rng = np.random.default_rng(9)
+    prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 8 + 3 * i)]
+               + [128009, 128260, 128261, 128257] for i in range(4)]
+    assert _compare_rows(cfg, w, prompts, 10) >= 0.8 * 4 * 10
