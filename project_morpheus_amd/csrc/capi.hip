@@ -86,6 +86,10 @@ struct mx_llm {
   float *h_dec = nullptr, *h_pre = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;
   float *part_ml = nullptr, *part_acc = nullptr;
   int* att_cnt = nullptr;
+  float* rows_ws = nullptr;     // split-K partial tiles of the multi-row GEMM
+  size_t rows_ws_floats = 0;
+  int* rows_tickets = nullptr;
+  size_t rows_tickets_n = 0;
   int nsplit_max = 0;
   int32_t *row_slot = nullptr, *row_pos = nullptr, *row_token = nullptr;
   int32_t *pre_slot = nullptr, *pre_pos = nullptr, *pre_ids = nullptr;
@@ -106,7 +110,8 @@ struct mx_llm {
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
   int att_cpw_batch = 2;        // option: same for multi-row (batched decode / prefill)
-  int gemv_wpb = 4;             // option: waves per block of the single-row GEMV
+  int gemv_wpb = 4;
+  int rows_ks = 0, rows_npart = 0;  // options: multi-row GEMM K chunk / activation parts             // option: waves per block of the single-row GEMV
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
 
   template <class T>
@@ -173,6 +178,22 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->part_ml, part_rows * c.heads * 2);
   A(x->part_acc, part_rows * c.heads * 128);
   A(x->att_cnt, (size_t)x->max_rows * c.kv_heads);
+  {  // multi-row GEMM workspace: the largest of the step's projections and the lm_head
+    const int Rm = x->max_rows;
+    const int shapes[5][4] = {{qkv_rows, c.hidden, Rm, EPI_QKV},
+                              {c.hidden, c.heads * 128, Rm, EPI_RESID},
+                              {2 * c.ffn, c.hidden, Rm, EPI_SILU},
+                              {c.hidden, c.ffn, Rm, EPI_RESID},
+                              {c.vocab, c.hidden, c.max_batch, EPI_ARGMAX}};
+    for (auto& sh : shapes) {
+      size_t wf = 0, tk = 0;
+      gemm_rows_workspace(sh[0], sh[1], sh[2], sh[3], &wf, &tk);
+      x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
+      x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
+    }
+  }
+  A(x->rows_ws, std::max<size_t>(x->rows_ws_floats, 1));
+  A(x->rows_tickets, x->rows_tickets_n);
   A(x->row_slot, c.max_batch);
   A(x->row_pos, c.max_batch);
   A(x->row_token, c.max_batch);
@@ -204,6 +225,7 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess) e = hipMemset(x->vcache, 0, x->kv_layer_elems * c.layers * 2);
   if (e == hipSuccess) e = hipMemset(x->best, 0, c.max_batch * 8);
   if (e == hipSuccess) e = hipMemset(x->att_cnt, 0, (size_t)x->max_rows * c.kv_heads * 4);
+  if (e == hipSuccess) e = hipMemset(x->rows_tickets, 0, x->rows_tickets_n * 4);
   if (e == hipSuccess) e = hipMemset(x->seen, 0, (size_t)slots * c.vocab);
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
   // every decode row starts parked on the scratch slot at position 0
@@ -370,6 +392,15 @@ struct RowSet {
   int max_len;  // upper bound of any row's position + 1 (sizes the attention grid)
 };
 
+static void attach_ws(mx_llm* x, GemvArgs& g) {
+  g.rows_ks = x->rows_ks;
+  g.rows_npart = x->rows_npart;
+  g.ws = x->rows_ws;
+  g.ws_floats = x->rows_ws_floats;
+  g.tickets = x->rows_tickets;
+  g.tickets_n = x->rows_tickets_n;
+}
+
 // Optional per-launch timing (eager runs only): prof->ev[k] brackets launch class k.
 enum { PK_QKV = 0, PK_ATTN, PK_O, PK_GU, PK_DOWN, PK_HEAD, PK_COMMIT, PK_N };
 struct Prof {
@@ -396,6 +427,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     uint16_t* kc = x->kcache + x->kv_layer_elems * li;
     uint16_t* vc = x->vcache + x->kv_layer_elems * li;
     GemvArgs g{};
+    attach_ws(x, g);
     g.R = rs.R;
     g.eps = c.eps;
     // QKV + RoPE + KV append
@@ -421,6 +453,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     if (e != hipSuccess) break;
     // O projection + residual
     GemvArgs o{};
+    attach_ws(x, o);
     o.R = rs.R; o.W = l.wo; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
     PROF_BEGIN(PK_O);
@@ -429,6 +462,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     if (e != hipSuccess) break;
     // gate/up + SiLU*up
     GemvArgs gu{};
+    attach_ws(x, gu);
     gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
     gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act; gu.force_legacy = x->legacy_gemv; gu.wpb = x->gemv_wpb; gu.rpw = x->rpw_gu;
     PROF_BEGIN(PK_GU);
@@ -437,6 +471,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     if (e != hipSuccess) break;
     // down + residual
     GemvArgs d{};
+    attach_ws(x, d);
     d.R = rs.R; d.W = l.wd; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
     d.ystride = H; d.force_legacy = x->legacy_gemv; d.wpb = x->gemv_wpb; d.rpw = x->rpw_down;
     PROF_BEGIN(PK_DOWN);
@@ -450,6 +485,7 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot, i
                                unsigned long long* best, hipStream_t st) {
   const auto& c = x->c;
   GemvArgs g{};
+  attach_ws(x, g);
   g.R = R; g.eps = c.eps; g.W = x->lm; g.N = c.vocab; g.K = c.hidden; g.X = h;
   g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
   g.penalty = x->penalty; g.best = best;
@@ -727,6 +763,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
+  } else if (k == "rows_ks") {
+    if (value != 0 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_ks must be 0 or 2");
+    x->rows_ks = value;
+  } else if (k == "rows_npart") {
+    if (value != 0 && value != 2 && value != 3) MX_FAIL(x, MX_ERR_ARG, "rows_npart must be 2 or 3");
+    x->rows_npart = value;
   } else if (k == "gemv_wpb") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "gemv_wpb must be 4 or 8");
     x->gemv_wpb = value;

@@ -23,10 +23,6 @@ namespace mx {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-}
-
 // x[0..7] -> NPART bf16x8 fragments with x = sum of parts (to fp32 rounding for NPART 3)
 template <int NPART>
 __device__ __forceinline__ void split_parts(float* x, bf16x8* f) {
@@ -35,124 +31,23 @@ __device__ __forceinline__ void split_parts(float* x, bf16x8* f) {
     uint32_t wv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float a = x[2 * j], b = x[2 * j + 1];
-      const uint16_t ha = f32_to_bf16(a), hb = f32_to_bf16(b);
-      wv[j] = (uint32_t)ha | ((uint32_t)hb << 16);
-      x[2 * j] = a - bf16_to_f32(ha);
-      x[2 * j + 1] = b - bf16_to_f32(hb);
+      const uint32_t pk = pack2_bf16(x[2 * j], x[2 * j + 1]);
+      wv[j] = pk;
+      if (p + 1 < NPART) {  // residual for the next part (exact in fp32)
+        x[2 * j] -= bf16_lo(pk);
+        x[2 * j + 1] -= bf16_hi(pk);
+      }
     }
     f[p] = __builtin_bit_cast(bf16x8, make_uint4(wv[0], wv[1], wv[2], wv[3]));
   }
 }
 
-template <int MT, int NT, int NPART, int EPI, bool NORM, int WK>
-__global__ __launch_bounds__(WK * 64) void gemm_rows_kernel(GemvArgs a) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * (16 * MT);
-  const int r0 = blockIdx.y * (16 * NT);
-  const int Kw = a.K / WK;
-  const int kbeg = w * Kw;
-
-  const uint4* wp[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int n = min(n0 + 16 * mt + c, a.N - 1);
-    wp[mt] = reinterpret_cast<const uint4*>(a.W + (size_t)n * a.K) + g;
-  }
-  const float* xp[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int b = min(r0 + 16 * nt + c, a.R - 1);
-    xp[nt] = a.X + (size_t)b * a.xstride + 8 * g;
-  }
-  const float* nwp = a.norm_w + 8 * g;
-
-  f32x4 acc[MT][NT];
-  float ss[NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) ss[nt] = 0.f;
-
-#pragma unroll 2
-  for (int k = kbeg; k < kbeg + Kw; k += 32) {
-    uint4 wv[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) wv[mt] = load_nt(wp[mt] + (k >> 3));
-    float4 xl[NT], xh[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      xl[nt] = *reinterpret_cast<const float4*>(xp[nt] + k);
-      xh[nt] = *reinterpret_cast<const float4*>(xp[nt] + k + 4);
-    }
-    float4 nl, nh;
-    if (NORM) {
-      nl = *reinterpret_cast<const float4*>(nwp + k);
-      nh = *reinterpret_cast<const float4*>(nwp + k + 4);
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      float x[8] = {xl[nt].x, xl[nt].y, xl[nt].z, xl[nt].w, xh[nt].x, xh[nt].y, xh[nt].z, xh[nt].w};
-      if (NORM) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss[nt] = fmaf(x[j], x[j], ss[nt]);
-        x[0] *= nl.x; x[1] *= nl.y; x[2] *= nl.z; x[3] *= nl.w;
-        x[4] *= nh.x; x[5] *= nh.y; x[6] *= nh.z; x[7] *= nh.w;
-      }
-      bf16x8 pf[NPART];
-      split_parts<NPART>(x, pf);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 wb = __builtin_bit_cast(bf16x8, wv[mt]);
-#pragma unroll
-        for (int p = 0; p < NPART; ++p)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, pf[p], acc[mt][nt], 0, 0, 0);
-      }
-    }
-  }
-
-  // ---- deterministic K-split reduction: waves 1.. -> LDS, wave 0 sums in wave order ----
-  __shared__ f32x4 red[WK - 1][MT * NT][64];
-  __shared__ float ssr[WK - 1][NT][64];
-  if (w > 0) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) red[w - 1][mt * NT + nt][lane] = acc[mt][nt];
-    if (NORM) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) ssr[w - 1][nt][lane] = ss[nt];
-    }
-  }
-  __syncthreads();
-  if (w != 0) return;
-#pragma unroll
-  for (int ww = 0; ww < WK - 1; ++ww) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] += red[ww][mt * NT + nt][lane];
-    if (NORM) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) ss[nt] += ssr[ww][nt][lane];
-    }
-  }
-  float scale[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    scale[nt] = 1.f;
-    if (NORM) {
-      float t = ss[nt];
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      scale[nt] = 1.0f / sqrtf(t / (float)a.K + a.eps);
-    }
-  }
-
-  // ---- epilogue: lane (batch col c, group g) holds weight rows 16 mt + 4 g + i ----------
+// Epilogue of one wave's tile: lane (batch col c, group g) holds weight rows
+// n0 + 16 mt + 4 g + i for batch rows r0 + 16 nt + c (MFMA C/D layout).
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT][NT],
+                                              const float (&scale)[NT], int n0, int r0, int c,
+                                              int g) {
   unsigned long long best[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) best[nt] = 0ull;
@@ -240,31 +135,282 @@ __global__ __launch_bounds__(WK * 64) void gemm_rows_kernel(GemvArgs a) {
   }
 }
 
-template <int MT, int NT, int EPI, bool NORM>
-static hipError_t launch_rows_t(const GemvArgs& a, hipStream_t st) {
-  constexpr int WK = 8;
-  const dim3 grid((a.N + 16 * MT - 1) / (16 * MT), (a.R + 16 * NT - 1) / (16 * NT));
-  hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, 3, EPI, NORM, WK>), grid, dim3(WK * 64), 0, st, a);
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One block = 8 waves; wave w owns weight rows n0 + 16 MT w .. (+16 MT) of the block's tile
+// and the tile's 16 NT batch rows, over the block's K range of SUB sub-chunks of 128.
+// Activations are shared, not re-read per wave: each sub-chunk of X is loaded ONCE per block
+// (one 32-byte piece per thread), RMS-norm-weighted, split into three bf16 parts and written
+// to LDS in MFMA B-fragment order (ds_read_b128, lane-linear, conflict-free); the weights
+// stream straight to registers one sub-chunk ahead.  Issue order per sub-chunk: X(s+1)
+// then W(s+1), so staging X(s+1) never waits behind the weight stream (vmcnt is in order).
+// K ranges (gridDim.y of them) give the grid its parallelism; each publishes its partial
+// tiles with write-through (sc1) stores, and the last arriving range sums them in range
+// order (deterministic) and runs the epilogue (MI355X_MICROARCH.md "Valid forms", row 1).
+template <int MT, int NT, int EPI, bool NORM, int SUB>
+__global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
+  constexpr int NP = 3, ST = 4;             // activation parts; k-steps per sub-chunk
+  constexpr int ITEMS = (NT * 16 * 16) / 512 > 0 ? (NT * 16 * 16) / 512 : 1;  // X pieces/thread
+  constexpr int WSLAB = MT * NT * 4 * 64;   // floats per wave partial
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (8 * 16 * MT) + w * 16 * MT;
+  const int kc = blockIdx.y, nkc = gridDim.y;
+  const int r0 = blockIdx.z * (16 * NT);
+  const int kr0 = kc * SUB * 128;
+
+  __shared__ uint4 xs[2][NP][NT][ST][64];
+  __shared__ float ssrow[16 * NT];
+  __shared__ int last_s;
+
+  // X piece of thread t (item it): batch row b = (t + 512 it) >> 4, 8 k at 8 ((t) & 15)
+  const bool xact = tid < NT * 16 * 16;
+  int xb[ITEMS], xj[ITEMS];
+  const float* xrow[ITEMS];
+#pragma unroll
+  for (int it = 0; it < ITEMS; ++it) {
+    const int q = tid + 512 * it;
+    xb[it] = min(q >> 4, 16 * NT - 1);
+    xj[it] = q & 15;
+    xrow[it] = a.X + (size_t)min(r0 + xb[it], a.R - 1) * a.xstride + 8 * xj[it];
+  }
+  const uint4* wrow[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int n = min(n0 + 16 * mt + c, a.N - 1);
+    wrow[mt] = reinterpret_cast<const uint4*>(a.W + (size_t)n * a.K) + g;
+  }
+  float ssp[ITEMS];
+#pragma unroll
+  for (int it = 0; it < ITEMS; ++it) ssp[it] = 0.f;
+
+  float4 xr[2][ITEMS][2], nr[2][ITEMS][2];
+  uint4 wv[2][ST][MT];
+  auto load_x = [&](int sub, int buf) {
+    const int k = kr0 + 128 * sub;
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      xr[buf][it][0] = *reinterpret_cast<const float4*>(xrow[it] + k);
+      xr[buf][it][1] = *reinterpret_cast<const float4*>(xrow[it] + k + 4);
+      if (NORM) {
+        const float* nw = a.norm_w + k + 8 * xj[it];
+        nr[buf][it][0] = *reinterpret_cast<const float4*>(nw);
+        nr[buf][it][1] = *reinterpret_cast<const float4*>(nw + 4);
+      }
+    }
+  };
+  auto load_w = [&](int sub, int buf) {
+    const int k8 = (kr0 + 128 * sub) >> 3;
+#pragma unroll
+    for (int st = 0; st < ST; ++st)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) wv[buf][st][mt] = load_nt(wrow[mt] + k8 + 4 * st);
+  };
+  auto stage_x = [&](int buf) {
+    if (!xact) return;
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      float x[8] = {xr[buf][it][0].x, xr[buf][it][0].y, xr[buf][it][0].z, xr[buf][it][0].w,
+                    xr[buf][it][1].x, xr[buf][it][1].y, xr[buf][it][1].z, xr[buf][it][1].w};
+      if (NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ssp[it] = fmaf(x[j], x[j], ssp[it]);
+        x[0] *= nr[buf][it][0].x; x[1] *= nr[buf][it][0].y;
+        x[2] *= nr[buf][it][0].z; x[3] *= nr[buf][it][0].w;
+        x[4] *= nr[buf][it][1].x; x[5] *= nr[buf][it][1].y;
+        x[6] *= nr[buf][it][1].z; x[7] *= nr[buf][it][1].w;
+      }
+      bf16x8 pf[NP];
+      split_parts<NP>(x, pf);
+      const int b = xb[it], j = xj[it];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        xs[buf][p][b >> 4][j >> 2][(j & 3) * 16 + (b & 15)] = __builtin_bit_cast(uint4, pf[p]);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_x(0, 0);
+  load_w(0, 0);
+  stage_x(0);
+  __syncthreads();
+#pragma unroll
+  for (int sub = 0; sub < SUB; ++sub) {
+    const int cur = sub & 1, nxt = cur ^ 1;
+    if (sub + 1 < SUB) {
+      load_x(sub + 1, nxt);
+      load_w(sub + 1, nxt);
+    }
+#pragma unroll
+    for (int st = 0; st < ST; ++st) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xs[cur][p][nt][st][lane]);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, wv[cur][st][mt]), xb8, acc[mt][nt], 0, 0, 0);
+        }
+      }
+    }
+    if (sub + 1 < SUB) stage_x(nxt);
+    __syncthreads();
+  }
+  // per-row sum of squares of this K range: the 16 threads of a row are 16 adjacent lanes
+  if (NORM) {
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      float t = ssp[it];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64);
+      if (xact && xj[it] == 0) ssrow[xb[it]] = t;
+    }
+    __syncthreads();
+  }
+  float ss[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) ss[nt] = NORM ? ssrow[16 * nt + c] : 0.f;
+
+  if (nkc > 1) {  // publish this K range's partial, last arriver merges in range order
+    const size_t tile = (size_t)blockIdx.z * gridDim.x + blockIdx.x;
+    const size_t slab_floats = 8 * (size_t)WSLAB + 16 * NT;
+    float* base = a.ws + tile * nkc * slab_floats;
+    float* mine = base + (size_t)kc * slab_floats;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          st_wt(mine + (size_t)w * WSLAB + ((mt * NT + nt) * 4 + i) * 64 + lane, acc[mt][nt][i]);
+    if (NORM && tid < 16 * NT) st_wt(mine + 8 * (size_t)WSLAB + tid, ssrow[tid]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == nkc - 1;
+      if (last) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ss[nt] = 0.f;
+    for (int q = 0; q < nkc; ++q) {
+      const float* src = base + (size_t)q * slab_floats;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[mt][nt][i] += ld_wt(src + (size_t)w * WSLAB + ((mt * NT + nt) * 4 + i) * 64 + lane);
+      if (NORM) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) ss[nt] += ld_wt(src + 8 * (size_t)WSLAB + 16 * nt + c);
+      }
+    }
+  }
+  float scale[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    scale[nt] = NORM ? 1.0f / sqrtf(ss[nt] / (float)a.K + a.eps) : 1.f;
+  rows_epilogue<MT, NT, EPI>(a, acc, scale, n0, r0, c, g);
+}
+
+// K ranges per launch: enough blocks to fill the chip without inflating the partial-tile
+// traffic (each range adds R x N x 4 bytes of write-through partials).
+static int rows_nkc(int N, int K, int R, int MT, int NT) {
+  const int subs = K / 128;
+  const int tiles = ((N + 128 * MT - 1) / (128 * MT)) * ((R + 16 * NT - 1) / (16 * NT));
+  int nkc = 1;
+  while (tiles * nkc < 384 && subs % (2 * nkc) == 0 && subs / (2 * nkc) >= 2) nkc *= 2;
+  while (tiles * nkc < 384 && subs % (3 * nkc) == 0 && subs / (3 * nkc) >= 2) nkc *= 3;
+  return nkc;
+}
+
+template <int MT, int NT, int EPI, bool NORM, int SUB>
+static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
+  const int tiles_n = (a.N + 128 * MT - 1) / (128 * MT), tiles_r = (a.R + 16 * NT - 1) / (16 * NT);
+  if (nkc > 1) {
+    const size_t need = (size_t)tiles_n * tiles_r * nkc * (8 * MT * NT * 4 * 64 + 16 * NT);
+    if (!a.ws || !a.tickets || need > a.ws_floats || (size_t)tiles_n * tiles_r > a.tickets_n)
+      return hipErrorInvalidValue;
+  }
+  const dim3 grid(tiles_n, nkc, tiles_r);
+  hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB>), grid, dim3(512), 0, st, a);
   return hipGetLastError();
+}
+
+template <int MT, int NT, int EPI, bool NORM>
+static hipError_t launch_rows_k(const GemvArgs& a, hipStream_t st) {
+  if (a.K % 128) return hipErrorNotSupported;
+  const int nkc = rows_nkc(a.N, a.K, a.R, MT, NT);
+  switch (a.K / 128 / nkc) {
+    case 1: return launch_rows_sub<MT, NT, EPI, NORM, 1>(a, nkc, st);
+    case 2: return launch_rows_sub<MT, NT, EPI, NORM, 2>(a, nkc, st);
+    case 3: return launch_rows_sub<MT, NT, EPI, NORM, 3>(a, nkc, st);
+    case 4: return launch_rows_sub<MT, NT, EPI, NORM, 4>(a, nkc, st);
+    case 6: return launch_rows_sub<MT, NT, EPI, NORM, 6>(a, nkc, st);
+    case 8: return launch_rows_sub<MT, NT, EPI, NORM, 8>(a, nkc, st);
+    case 12: return launch_rows_sub<MT, NT, EPI, NORM, 12>(a, nkc, st);
+    case 16: return launch_rows_sub<MT, NT, EPI, NORM, 16>(a, nkc, st);
+    case 24: return launch_rows_sub<MT, NT, EPI, NORM, 24>(a, nkc, st);
+    default: return hipErrorNotSupported;
+  }
+}
+
+static void rows_tiles(int epi, int R, int* mt, int* nt) {
+  *nt = R <= 16 ? 1 : R <= 32 ? 2 : 4;
+  *mt = 1;
+}
+
+// Workspace (floats) and tickets a launch of this shape needs (0 when K is one range).
+void gemm_rows_workspace(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets) {
+  int mt, nt;
+  rows_tiles(epi, R, &mt, &nt);
+  const int nkc = K % 128 ? 1 : rows_nkc(N, K, R, mt, nt);
+  const size_t tn = (N + 128 * mt - 1) / (128 * mt), tr = (R + 16 * nt - 1) / (16 * nt);
+  *ws_floats = nkc > 1 ? tn * tr * nkc * (8 * (size_t)mt * nt * 4 * 64 + 16 * nt) : 0;
+  *tickets = tn * tr;
 }
 
 // R >= 2 rows.  Returns hipErrorNotSupported for shapes the kernel does not cover.
 hipError_t launch_gemm_rows(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
-  if (a.K % (32 * 8) || a.R < 1) return hipErrorNotSupported;
-  const int nt = a.R <= 16 ? 1 : a.R <= 32 ? 2 : 4;
-  // 64-row tiles carry half the weight rows per wave (register budget: no spills)
-#define MX_R(MT_, EPI_, NORM_)                                                            \
+  if (a.R < 1) return hipErrorNotSupported;
+  int mt, nt;
+  rows_tiles(epi, a.R, &mt, &nt);
+#define MX_R(EPI_, NORM_)                                                                 \
   if (epi == EPI_ && norm == NORM_) {                                                     \
-    if (nt == 1) return launch_rows_t<MT_, 1, EPI_, NORM_>(a, st);                        \
-    if (nt == 2) return launch_rows_t<MT_, 2, EPI_, NORM_>(a, st);                        \
-    return launch_rows_t<(MT_ > 1 ? MT_ / 2 : 1), 4, EPI_, NORM_>(a, st);                 \
+    if (nt == 1) return launch_rows_k<1, 1, EPI_, NORM_>(a, st);                          \
+    if (nt == 2) return launch_rows_k<1, 2, EPI_, NORM_>(a, st);                          \
+    return launch_rows_k<1, 4, EPI_, NORM_>(a, st);                                       \
   }
-  MX_R(2, EPI_QKV, true)
-  MX_R(1, EPI_RESID, false)
-  MX_R(2, EPI_SILU, true)
-  MX_R(4, EPI_ARGMAX, true)
-  MX_R(2, EPI_STORE, false)
-  MX_R(2, EPI_STORE, true)
+  MX_R(EPI_QKV, true)
+  MX_R(EPI_RESID, false)
+  MX_R(EPI_SILU, true)
+  MX_R(EPI_ARGMAX, true)
+  MX_R(EPI_STORE, false)
+  MX_R(EPI_STORE, true)
 #undef MX_R
   return hipErrorNotSupported;
 }

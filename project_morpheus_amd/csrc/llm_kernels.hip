@@ -375,21 +375,16 @@ __device__ __forceinline__ void st_wt(float* p, float v) {
 __device__ __forceinline__ float ld_wt(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-}
 // x = p0 + p1 + p2 with p_i bf16 (exact to fp32 rounding); 8 values -> three fragments
 __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, bf16x8& f2) {
   uint32_t w0[4], w1[4], w2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float a = x[2 * j], b = x[2 * j + 1];
-    const float a0 = bf16_to_f32(f32_to_bf16(a)), b0 = bf16_to_f32(f32_to_bf16(b));
-    const float a1 = a - a0, b1 = b - b0;
-    const float a1r = bf16_to_f32(f32_to_bf16(a1)), b1r = bf16_to_f32(f32_to_bf16(b1));
-    w0[j] = pack_bf16(a0, b0);
-    w1[j] = pack_bf16(a1r, b1r);
-    w2[j] = pack_bf16(a1 - a1r, b1 - b1r);
+    const float a = x[2 * j], b = x[2 * j + 1];
+    w0[j] = pack2_bf16(a, b);
+    const float a1 = a - bf16_lo(w0[j]), b1 = b - bf16_hi(w0[j]);
+    w1[j] = pack2_bf16(a1, b1);
+    w2[j] = pack2_bf16(a1 - bf16_lo(w1[j]), b1 - bf16_hi(w1[j]));
   }
   f0 = __builtin_bit_cast(bf16x8, make_uint4(w0[0], w0[1], w0[2], w0[3]));
   f1 = __builtin_bit_cast(bf16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));

@@ -13,10 +13,17 @@ __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 // fp32 -> bf16 round-to-nearest-even (matches torch .bfloat16() for finite values).
+// A plain cast lowers to the hardware v_cvt_pk_bf16_f32 on gfx950 (MI355X_MICROARCH.md
+// "Correctness boundaries": it also keeps NaNs NaN, unlike the integer-rounding trick).
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// two fp32 -> packed bf16x2 (lo in bits 0-15), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack2_bf16(float lo, float hi) {
+  const bf16x2_t v = __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -26,6 +26,12 @@ struct GemvArgs {
   int force_legacy;        // 1: use the grid-stride kernel even for R = 1 (A/B timing)
   int wpb;                 // R = 1 kernel: waves per block (4 or 8; 0 = 8)
   int rpw;                 // R = 1 kernel: weight rows per wave (0 = default per epilogue)
+  float* ws;               // R >= 2 kernel: split-K partial tiles (gemm_rows_workspace)
+  size_t ws_floats;
+  int* tickets;            // R >= 2 kernel: per-tile arrival counters (zero between launches)
+  size_t tickets_n;
+  int rows_ks;             // R >= 2 kernel: 2 = 512-wide K chunks (0 = default)
+  int rows_npart;          // R >= 2 kernel: activation bf16 parts (2 or 3; 0 = 3)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -77,6 +83,7 @@ hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 // R >= 2 rows on bf16 MFMA (llm_batched.hip); hipErrorNotSupported if the shape is not covered
 hipError_t launch_gemm_rows(const GemvArgs& a, int epi, bool norm, hipStream_t st);
+void gemm_rows_workspace(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);

@@ -14,13 +14,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0,
-            "rpw_down": 0}
+DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 2, "gemv_wpb": 4, "rpw_o": 0,
+            "rpw_gu": 0, "rpw_down": 0, "rows_ks": 0, "rows_npart": 0}
 VARIANTS = {
     "base": {},
     "att_cpw2": {"att_cpw": 2},
     "att_cpw4": {"att_cpw": 4},
     "rpw_gu4": {"rpw_gu": 4},
+    "att_cpw_batch1": {"att_cpw_batch": 1},
+    "rows_ks2": {"rows_ks": 2},
+    "rows_np2": {"rows_npart": 2},
+    "rows_ks2_np2": {"rows_ks": 2, "rows_npart": 2},
+    "att_cpw_batch4": {"att_cpw_batch": 4},
 }
 
 
@@ -30,6 +35,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--rows", type=int, default=1)
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -37,7 +43,8 @@ def main():
     from project_morpheus_amd.weights import synthetic_llm_weights
     cfg = C.OrpheusConfig()
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
-    llm = LlmEngine(cfg, w, device=0, max_slots=1, max_pos=2048, max_batch=1, max_prefill=256)
+    R = args.rows
+    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=256)
     del w
     torch.cuda.empty_cache()
     st = torch.cuda.Stream()
@@ -49,17 +56,19 @@ def main():
             opts = dict(DEFAULTS, **VARIANTS[name])
             for k, v in opts.items():
                 llm.set_option(k, v)
-            llm.prefill(0, 0, prompt, 1.1, st)
+            for r in range(R):
+                llm.prefill(r, r, prompt, 1.1, st)
             for _ in range(args.pos - len(prompt)):
-                llm.decode(1, 1.1, st)
+                llm.decode(R, 1.1, st)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(args.reps):
-                llm.decode(1, 1.1, st)
+                llm.decode(R, 1.1, st)
             e1.record(st)
             e1.synchronize()
             res[name].append(round(e0.elapsed_time(e1) / args.reps, 4))
-            llm.release_row(0, st)
+            for r in range(R):
+                llm.release_row(r, st)
             st.synchronize()
         print(f"round {rnd}: " + json.dumps({n: res[n][-1] for n in names}), flush=True)
     print(json.dumps({n: {"median_ms": statistics.median(v), "all": v} for n, v in res.items()},
