@@ -37,6 +37,10 @@ extern "C" {
 
 #define MX_DTYPE_F32 0
 #define MX_DTYPE_BF16 1
+#define MX_DTYPE_FP8 2   /* OCP e4m3 (e4m3fn) bytes */
+
+#define MX_WEIGHTS_BF16 0
+#define MX_WEIGHTS_FP8 1 /* e4m3 matrices + one fp32 dequant scale per output row */
 
 typedef struct mx_llm mx_llm;
 typedef struct mx_snac mx_snac;
@@ -50,6 +54,7 @@ typedef struct mx_llm_config {
   int32_t max_prefill;  /* prompt tokens per prefill call */
   float eps;            /* RMSNorm eps (1e-5) */
   int32_t tied;         /* lm_head shares the embedding table */
+  int32_t wdtype;       /* MX_WEIGHTS_BF16 | MX_WEIGHTS_FP8 (BASELINE configs[4]) */
 } mx_llm_config;
 
 /* ---- library / memory -------------------------------------------------------------- */
@@ -59,7 +64,10 @@ int mx_host_free(void* host_ptr);
 
 /* ---- LLM decoder (replaces vLLM / llama.cpp decode) -------------------------------- */
 int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out);
-/* names: embed, norm, lm_head (untied), l{i}.{attn_norm,wq,wk,wv,wo,mlp_norm,wg,wu,wd} */
+/* names: embed, norm, lm_head (untied), l{i}.{attn_norm,wq,wk,wv,wo,mlp_norm,wg,wu,wd}.
+ * MX_WEIGHTS_FP8 engines: every matrix but embed comes as MX_DTYPE_FP8 bytes plus
+ * "<name>.scale" (fp32, one per output row: W = scale[row] * e4m3); lm_head is always given
+ * (the tied embedding stays bf16 for the token lookup). */
 int mx_llm_set_weight(mx_llm* ctx, const char* name, const void* dev_data, int64_t numel,
                       int dtype);
 /* RoPE tables [n_pos][head_dim/2] fp32 (host memory), llama3-scaled frequencies. */

@@ -18,6 +18,9 @@ LIB_PATH = os.environ.get("MORPHEUS_MX_LIB", os.path.join(HERE, "libmorpheus_mx.
 
 MX_DTYPE_F32 = 0
 MX_DTYPE_BF16 = 1
+MX_DTYPE_FP8 = 2      # OCP e4m3 bytes
+
+MX_WEIGHTS = {"bf16": 0, "fp8": 1}
 
 
 class MxUnavailable(RuntimeError):
@@ -32,7 +35,7 @@ class LlmConfig(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "hidden", "layers", "heads", "kv_heads", "head_dim", "ffn", "vocab",
         "max_slots", "max_pos", "max_batch", "max_prefill")] + [
-        ("eps", C.c_float), ("tied", C.c_int32)]
+        ("eps", C.c_float), ("tied", C.c_int32), ("wdtype", C.c_int32)]
 
 
 _P = C.c_void_p

@@ -35,16 +35,19 @@ def needs_build() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
-    objs = []
-    for s in SOURCES:
+    objs, procs = [], []
+    for s in SOURCES:  # translation units compile in parallel
         src = os.path.join(CSRC, s)
         obj = os.path.join(CSRC, s.replace(".hip", ".o"))
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                "-munsafe-fp-atomics", "-Wno-unused-result", "-x", "hip", "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = LIB + ".tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)

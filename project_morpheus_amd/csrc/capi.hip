@@ -58,14 +58,17 @@ extern "C" int mx_host_free(void* host_ptr) {
 // =====================================================================================
 // LLM context
 // =====================================================================================
+// Weight matrices are bf16, or OCP e4m3 bytes + one fp32 dequant scale per packed row
+// (mx_llm_config.wdtype); the packed row order serves the kernels' epilogues.
 struct LayerW {
   float* attn_norm = nullptr;
   float* mlp_norm = nullptr;
-  uint16_t* wqkv = nullptr;  // [(H + 2*kvh*128)][H], q/k rows pair-interleaved for RoPE
-  uint16_t* wo = nullptr;    // [H][heads*128]
-  uint16_t* wgu = nullptr;   // [2F][H], rows (gate_i, up_i) interleaved
-  uint16_t* wd = nullptr;    // [H][F]
-  unsigned loaded = 0;
+  void* wqkv = nullptr;  // [(H + 2*kvh*128)][H], q/k rows pair-interleaved for RoPE
+  void* wo = nullptr;    // [H][heads*128]
+  void* wgu = nullptr;   // [2F][H], rows (gate_i, up_i) interleaved
+  void* wd = nullptr;    // [H][F]
+  float *sqkv = nullptr, *so = nullptr, *sgu = nullptr, *sd = nullptr;  // fp8 row scales
+  unsigned loaded = 0, scaled = 0;
 };
 
 struct mx_llm {
@@ -73,8 +76,11 @@ struct mx_llm {
   mx_llm_config c{};
   std::string err;
   std::vector<void*> allocs;
-  uint16_t* embed = nullptr;
-  uint16_t* lm = nullptr;
+  uint16_t* embed = nullptr;   // bf16 always (token embedding gather)
+  void* lm = nullptr;          // lm_head: the embedding (tied bf16) or its own matrix
+  float* slm = nullptr;        // fp8 lm_head row scales
+  bool lm_loaded = false, lm_scaled = false;
+  int esz = 2;                 // bytes per matrix element (2 bf16, 1 fp8)
   float* norm = nullptr;
   std::vector<LayerW> L;
   float* rope_cos = nullptr;
@@ -143,6 +149,9 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (c.heads * 128 % 256) return bad("heads*128 must be a multiple of 256");
   if (c.max_pos % 128) return bad("max_pos must be a multiple of 128");
   if (c.max_batch < 1 || c.max_prefill < 1 || c.max_slots < 1) return bad("bad limits");
+  if (c.wdtype != WT_BF16 && c.wdtype != WT_FP8) return bad("bad wdtype");
+  if (c.wdtype == WT_FP8 && (c.hidden % 1024 || c.ffn % 1024 || c.heads * 128 % 1024))
+    return bad("fp8 needs hidden, ffn and heads*128 multiples of 1024");
   if (hipSetDevice(device) != hipSuccess) return bad("hipSetDevice failed");
   x->L.resize(c.layers);
   x->pos_mirror.assign(c.max_batch, 0);
@@ -155,17 +164,33 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   hipError_t e = hipSuccess;
 #define A(p, n) \
   if (e == hipSuccess) e = x->alloc(&(p), (size_t)(n));
+  const bool f8 = c.wdtype == WT_FP8;
+  x->esz = f8 ? 1 : 2;
+  uint8_t* m8 = nullptr;  // byte-typed allocations of matrices
+#define AM(p, rows, cols)                                                  \
+  if (e == hipSuccess) {                                                   \
+    e = x->alloc(&m8, (size_t)(rows) * (cols) * x->esz);                  \
+    p = m8;                                                                \
+  }
   A(x->embed, (size_t)c.vocab * c.hidden);
-  if (!c.tied) A(x->lm, (size_t)c.vocab * c.hidden);
+  if (!c.tied || f8) AM(x->lm, c.vocab, c.hidden);
+  if (f8) A(x->slm, c.vocab);
   A(x->norm, c.hidden);
   for (auto& l : x->L) {
     A(l.attn_norm, c.hidden);
     A(l.mlp_norm, c.hidden);
-    A(l.wqkv, (size_t)qkv_rows * c.hidden);
-    A(l.wo, (size_t)c.hidden * c.heads * 128);
-    A(l.wgu, (size_t)2 * c.ffn * c.hidden);
-    A(l.wd, (size_t)c.hidden * c.ffn);
+    AM(l.wqkv, qkv_rows, c.hidden);
+    AM(l.wo, c.hidden, c.heads * 128);
+    AM(l.wgu, 2 * c.ffn, c.hidden);
+    AM(l.wd, c.hidden, c.ffn);
+    if (f8) {
+      A(l.sqkv, qkv_rows);
+      A(l.so, c.hidden);
+      A(l.sgu, 2 * c.ffn);
+      A(l.sd, c.hidden);
+    }
   }
+#undef AM
   A(x->kcache, x->kv_layer_elems * c.layers);
   A(x->vcache, x->kv_layer_elems * c.layers);
   A(x->h_dec, (size_t)c.max_batch * c.hidden);
@@ -204,7 +229,7 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->seen, (size_t)slots * c.vocab);
   A(x->penalty, 1);
 #undef A
-  if (c.tied) x->lm = x->embed;
+  if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
     g_err = std::string("allocation failed: ") + hipGetErrorString(e);
     for (void* p : x->allocs) (void)hipFree(p);
@@ -246,114 +271,127 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   return MX_OK;
 }
 
-// q/k rows of each head are reordered so that packed rows (2i, 2i+1) hold the RoPE
-// partners (i, i+64); v rows keep their order.  gate/up rows are interleaved (g_i, u_i).
-static int pack_rows(mx_llm* x, uint16_t* dst, const void* src, const std::vector<int32_t>& perm,
-                     int cols, int dtype) {
-  int32_t* dperm = nullptr;
-  MX_TRY(x, hipMalloc(&dperm, perm.size() * 4));
-  MX_TRY(x, hipMemcpy(dperm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice));
-  hipError_t e = launch_pack_rows(dst, src, dperm, (int)perm.size(), cols,
-                                  dtype == MX_DTYPE_F32 ? 1 : 0, nullptr);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  (void)hipFree(dperm);
-  MX_TRY(x, e);
-  return MX_OK;
-}
+// Packing: source row i of a named matrix lands on packed row dmap[i] of its target:
+// q/k rows of each head go to (2i, 2i+1) <- (i, i+64) so the RoPE epilogue sees both
+// partners in one wave; gate/up rows are interleaved (g_i -> 2i, u_i -> 2i+1) so SiLU*up
+// is a per-wave epilogue; v/o/down/embed/lm_head keep their order.  fp8 row scales
+// ("<name>.scale") follow the same map.
+struct PackTarget {
+  void* base = nullptr;   // matrix storage
+  float* scale = nullptr; // fp8 scales of the same packed rows
+  std::vector<int32_t> dmap;
+  int cols = 0;
+  unsigned bit = 0;       // LayerW::loaded / scaled bit
+};
 
-static int copy_f32(mx_llm* x, float* dst, const void* src, int64_t n, int dtype) {
-  MX_TRY(x, launch_to_f32(dst, src, n, dtype == MX_DTYPE_BF16 ? 1 : 0, nullptr));
-  MX_TRY(x, hipDeviceSynchronize());
-  return MX_OK;
+static bool pack_target(mx_llm* x, const std::string& nm, PackTarget& t, LayerW** lw) {
+  const auto& c = x->c;
+  const int H = c.hidden, F = c.ffn, QD = c.heads * 128, KD = c.kv_heads * 128;
+  auto seq = [](int rows, int row0, int step) {
+    std::vector<int32_t> p(rows);
+    for (int i = 0; i < rows; ++i) p[i] = row0 + step * i;
+    return p;
+  };
+  auto qk = [](int heads, int row0) {
+    std::vector<int32_t> p(heads * 128);
+    for (int h = 0; h < heads; ++h)
+      for (int i = 0; i < 64; ++i) {
+        p[h * 128 + i] = row0 + h * 128 + 2 * i;
+        p[h * 128 + i + 64] = row0 + h * 128 + 2 * i + 1;
+      }
+    return p;
+  };
+  *lw = nullptr;
+  if (nm == "embed") { t.base = x->embed; t.dmap = seq(c.vocab, 0, 1); t.cols = H; return true; }
+  if (nm == "lm_head") {
+    t.base = x->lm; t.scale = x->slm; t.dmap = seq(c.vocab, 0, 1); t.cols = H; return true;
+  }
+  int li = -1;
+  char field[32] = {0};
+  if (std::sscanf(nm.c_str(), "l%d.%31s", &li, field) != 2 || li < 0 || li >= c.layers) return false;
+  LayerW& l = x->L[li];
+  *lw = &l;
+  const std::string f(field);
+  if (f == "wq") { t.base = l.wqkv; t.scale = l.sqkv; t.dmap = qk(c.heads, 0); t.cols = H; t.bit = 4; }
+  else if (f == "wk") { t.base = l.wqkv; t.scale = l.sqkv; t.dmap = qk(c.kv_heads, QD); t.cols = H; t.bit = 8; }
+  else if (f == "wv") { t.base = l.wqkv; t.scale = l.sqkv; t.dmap = seq(KD, QD + KD, 1); t.cols = H; t.bit = 16; }
+  else if (f == "wo") { t.base = l.wo; t.scale = l.so; t.dmap = seq(H, 0, 1); t.cols = QD; t.bit = 32; }
+  else if (f == "wg") { t.base = l.wgu; t.scale = l.sgu; t.dmap = seq(F, 0, 2); t.cols = H; t.bit = 64; }
+  else if (f == "wu") { t.base = l.wgu; t.scale = l.sgu; t.dmap = seq(F, 1, 2); t.cols = H; t.bit = 128; }
+  else if (f == "wd") { t.base = l.wd; t.scale = l.sd; t.dmap = seq(H, 0, 1); t.cols = F; t.bit = 256; }
+  else return false;
+  return true;
 }
 
 extern "C" int mx_llm_set_weight(mx_llm* x, const char* name, const void* data, int64_t numel,
                                  int dtype) {
   if (!x || !name || !data) return MX_ERR_ARG;
-  if (dtype != MX_DTYPE_F32 && dtype != MX_DTYPE_BF16) MX_FAIL(x, MX_ERR_ARG, "bad dtype");
+  if (dtype != MX_DTYPE_F32 && dtype != MX_DTYPE_BF16 && dtype != MX_DTYPE_FP8)
+    MX_FAIL(x, MX_ERR_ARG, "bad dtype");
   MX_TRY(x, hipSetDevice(x->device));
   const auto& c = x->c;
-  const int H = c.hidden, F = c.ffn, QD = c.heads * 128, KD = c.kv_heads * 128;
-  const std::string n(name);
-  auto need = [&](int64_t want) { return numel == want; };
-  auto ident = [](int rows) {
-    std::vector<int32_t> p(rows);
-    for (int i = 0; i < rows; ++i) p[i] = i;
-    return p;
-  };
-  if (n == "embed" || n == "lm_head") {
-    if (!need((int64_t)c.vocab * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    if (n == "lm_head" && c.tied) MX_FAIL(x, MX_ERR_ARG, "lm_head given but config is tied");
-    return pack_rows(x, n == "embed" ? x->embed : x->lm, data, ident(c.vocab), H, dtype);
-  }
+  const int H = c.hidden;
+  const bool f8 = c.wdtype == WT_FP8;
+  std::string n(name);
   if (n == "norm") {
-    if (!need(H)) MX_FAIL(x, MX_ERR_ARG, "norm: bad numel");
-    return copy_f32(x, x->norm, data, H, dtype);
+    if (numel != H) MX_FAIL(x, MX_ERR_ARG, "norm: bad numel");
+    MX_TRY(x, launch_to_f32(x->norm, data, H, dtype == MX_DTYPE_BF16 ? 1 : 0, nullptr));
+    MX_TRY(x, hipDeviceSynchronize());
+    return MX_OK;
   }
   int li = -1;
   char field[32] = {0};
-  if (std::sscanf(name, "l%d.%31s", &li, field) != 2 || li < 0 || li >= c.layers)
-    MX_FAIL(x, MX_ERR_ARG, "unknown weight " + n);
-  LayerW& l = x->L[li];
-  const std::string f(field);
-  // q/k/v are staged into one packed [qkv_rows][H] matrix at row offsets 0 / QD / QD+KD
-  auto qk_perm = [&](int heads) {
-    std::vector<int32_t> p(heads * 128);
-    for (int h = 0; h < heads; ++h)
-      for (int i = 0; i < 64; ++i) {
-        p[h * 128 + 2 * i] = h * 128 + i;
-        p[h * 128 + 2 * i + 1] = h * 128 + i + 64;
-      }
-    return p;
-  };
-  int rc = MX_OK;
-  if (f == "attn_norm" || f == "mlp_norm") {
-    if (!need(H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = copy_f32(x, f == "attn_norm" ? l.attn_norm : l.mlp_norm, data, H, dtype);
-    l.loaded |= f == "attn_norm" ? 1u : 2u;
-  } else if (f == "wq") {
-    if (!need((int64_t)QD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = pack_rows(x, l.wqkv, data, qk_perm(c.heads), H, dtype);
-    l.loaded |= 4u;
-  } else if (f == "wk") {
-    if (!need((int64_t)KD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = pack_rows(x, l.wqkv + (size_t)QD * H, data, qk_perm(c.kv_heads), H, dtype);
-    l.loaded |= 8u;
-  } else if (f == "wv") {
-    if (!need((int64_t)KD * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = pack_rows(x, l.wqkv + (size_t)(QD + KD) * H, data, ident(KD), H, dtype);
-    l.loaded |= 16u;
-  } else if (f == "wo") {
-    if (!need((int64_t)H * QD)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = pack_rows(x, l.wo, data, ident(H), QD, dtype);
-    l.loaded |= 32u;
-  } else if (f == "wg" || f == "wu") {
-    if (!need((int64_t)F * H)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    // gate row i -> packed row 2i, up row i -> packed row 2i+1: pack into a temporary
-    // [F][H] then scatter with a strided view (two passes of the row-copy kernel)
-    std::vector<int32_t> p(F);
-    for (int i = 0; i < F; ++i) p[i] = i;
-    uint16_t* tmp = nullptr;
-    MX_TRY(x, hipMalloc(&tmp, (size_t)F * H * 2));
-    rc = pack_rows(x, tmp, data, p, H, dtype);
-    if (rc == MX_OK) {
-      const int off = f == "wg" ? 0 : 1;
-      hipError_t e = hipMemcpy2D(l.wgu + (size_t)off * H, (size_t)2 * H * 2, tmp, (size_t)H * 2,
-                                 (size_t)H * 2, F, hipMemcpyDeviceToDevice);
-      (void)hipFree(tmp);
-      MX_TRY(x, e);
-    } else {
-      (void)hipFree(tmp);
-    }
-    l.loaded |= f == "wg" ? 64u : 128u;
-  } else if (f == "wd") {
-    if (!need((int64_t)H * F)) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
-    rc = pack_rows(x, l.wd, data, ident(H), F, dtype);
-    l.loaded |= 256u;
-  } else {
-    MX_FAIL(x, MX_ERR_ARG, "unknown weight " + n);
+  if (std::sscanf(name, "l%d.%31s", &li, field) == 2 && li >= 0 && li < c.layers &&
+      (std::string(field) == "attn_norm" || std::string(field) == "mlp_norm")) {
+    if (numel != H) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+    LayerW& l = x->L[li];
+    const bool an = std::string(field) == "attn_norm";
+    MX_TRY(x, launch_to_f32(an ? l.attn_norm : l.mlp_norm, data, H, dtype == MX_DTYPE_BF16 ? 1 : 0,
+                            nullptr));
+    MX_TRY(x, hipDeviceSynchronize());
+    l.loaded |= an ? 1u : 2u;
+    return MX_OK;
   }
-  return rc;
+  const bool is_scale = n.size() > 6 && n.compare(n.size() - 6, 6, ".scale") == 0;
+  if (is_scale) n = n.substr(0, n.size() - 6);
+  PackTarget t;
+  LayerW* lw = nullptr;
+  if (!pack_target(x, n, t, &lw)) MX_FAIL(x, MX_ERR_ARG, "unknown weight " + std::string(name));
+  const int rows = (int)t.dmap.size();
+  if (n == "lm_head" && c.tied && !f8) MX_FAIL(x, MX_ERR_ARG, "lm_head given but config is tied");
+  if (is_scale) {  // fp8 dequant scales [rows] fp32, host-permuted into packed order
+    if (!f8 || n == "embed") MX_FAIL(x, MX_ERR_ARG, n + ".scale only exists for fp8 matrices");
+    if (numel != rows || dtype != MX_DTYPE_F32) MX_FAIL(x, MX_ERR_ARG, n + ".scale: bad shape/dtype");
+    std::vector<float> src(rows), dst;
+    MX_TRY(x, hipMemcpy(src.data(), data, rows * 4, hipMemcpyDeviceToHost));
+    // rows of one target may be spread (interleaved): write through the map
+    std::vector<float> cur;
+    int lo = *std::min_element(t.dmap.begin(), t.dmap.end());
+    int hi = *std::max_element(t.dmap.begin(), t.dmap.end());
+    cur.resize(hi - lo + 1);
+    MX_TRY(x, hipMemcpy(cur.data(), t.scale + lo, cur.size() * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < rows; ++i) cur[t.dmap[i] - lo] = src[i];
+    MX_TRY(x, hipMemcpy(t.scale + lo, cur.data(), cur.size() * 4, hipMemcpyHostToDevice));
+    if (lw) lw->scaled |= t.bit;
+    else x->lm_scaled = true;
+    return MX_OK;
+  }
+  if ((int64_t)rows * t.cols != numel) MX_FAIL(x, MX_ERR_ARG, n + ": bad numel");
+  const bool want_f8 = f8 && n != "embed";
+  if (want_f8 != (dtype == MX_DTYPE_FP8))
+    MX_FAIL(x, MX_ERR_ARG, n + (want_f8 ? ": fp8 engine expects e4m3 bytes (+ .scale)"
+                                        : ": bf16/f32 expected"));
+  int32_t* dmap = nullptr;
+  MX_TRY(x, hipMalloc(&dmap, rows * 4));
+  hipError_t e = hipMemcpy(dmap, t.dmap.data(), rows * 4, hipMemcpyHostToDevice);
+  const int mode = dtype == MX_DTYPE_FP8 ? 2 : dtype == MX_DTYPE_F32 ? 1 : 0;
+  if (e == hipSuccess) e = launch_scatter_rows(t.base, data, dmap, rows, t.cols, mode, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  (void)hipFree(dmap);
+  MX_TRY(x, e);
+  if (lw) lw->loaded |= t.bit;
+  else if (n == "lm_head") x->lm_loaded = true;
+  return MX_OK;
 }
 
 extern "C" int mx_llm_set_rope(mx_llm* x, const float* cos_h, const float* sin_h, int n_pos) {
@@ -375,9 +413,15 @@ extern "C" int mx_llm_set_rope(mx_llm* x, const float* cos_h, const float* sin_h
 
 extern "C" int mx_llm_finalize(mx_llm* x) {
   if (!x) return MX_ERR_ARG;
-  for (int i = 0; i < x->c.layers; ++i)
+  const bool f8 = x->c.wdtype == WT_FP8;
+  for (int i = 0; i < x->c.layers; ++i) {
     if (x->L[i].loaded != 511u)
       MX_FAIL(x, MX_ERR_STATE, "layer " + std::to_string(i) + " weights incomplete");
+    if (f8 && x->L[i].scaled != 508u)
+      MX_FAIL(x, MX_ERR_STATE, "layer " + std::to_string(i) + " fp8 scales incomplete");
+  }
+  if ((!x->c.tied || f8) && !x->lm_loaded) MX_FAIL(x, MX_ERR_STATE, "lm_head not loaded");
+  if (f8 && !x->lm_scaled) MX_FAIL(x, MX_ERR_STATE, "lm_head fp8 scales not loaded");
   if (!x->rope_cos) MX_FAIL(x, MX_ERR_STATE, "rope table not set");
   x->final = true;
   return MX_OK;
@@ -431,7 +475,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     g.R = rs.R;
     g.eps = c.eps;
     // QKV + RoPE + KV append
-    g.W = l.wqkv; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
+    g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
     g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
@@ -454,7 +498,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // O projection + residual
     GemvArgs o{};
     attach_ws(x, o);
-    o.R = rs.R; o.W = l.wo; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
+    o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
     PROF_BEGIN(PK_O);
     e = launch_gemv(o, EPI_RESID, false, st);
@@ -463,7 +507,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // gate/up + SiLU*up
     GemvArgs gu{};
     attach_ws(x, gu);
-    gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
+    gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.wscale = l.sgu; gu.wdtype = c.wdtype; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
     gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act; gu.force_legacy = x->legacy_gemv; gu.wpb = x->gemv_wpb; gu.rpw = x->rpw_gu;
     PROF_BEGIN(PK_GU);
     e = launch_gemv(gu, EPI_SILU, true, st);
@@ -472,7 +516,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // down + residual
     GemvArgs d{};
     attach_ws(x, d);
-    d.R = rs.R; d.W = l.wd; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
+    d.R = rs.R; d.W = l.wd; d.wscale = l.sd; d.wdtype = c.wdtype; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
     d.ystride = H; d.force_legacy = x->legacy_gemv; d.wpb = x->gemv_wpb; d.rpw = x->rpw_down;
     PROF_BEGIN(PK_DOWN);
     e = launch_gemv(d, EPI_RESID, false, st);
@@ -486,7 +530,7 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot, i
   const auto& c = x->c;
   GemvArgs g{};
   attach_ws(x, g);
-  g.R = R; g.eps = c.eps; g.W = x->lm; g.N = c.vocab; g.K = c.hidden; g.X = h;
+  g.R = R; g.eps = c.eps; g.W = x->lm; g.wscale = x->slm; g.wdtype = c.wdtype; g.N = c.vocab; g.K = c.hidden; g.X = h;
   g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
   g.penalty = x->penalty; g.best = best;
   g.logits = x->logits_dbg ? x->logits_dbg + (size_t)(best - x->best) * c.vocab : nullptr;
@@ -708,18 +752,18 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int reps, float* us_out,
     GemvArgs g{};
     g.R = 1; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
     if (which == 0) {
-      g.W = l.wqkv; g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
+      g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
       g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = x->row_slot;
       g.row_pos = x->row_pos; g.kcache = x->kcache + x->kv_layer_elems * li;
       g.vcache = x->vcache + x->kv_layer_elems * li; g.heads = c.heads; g.kv_heads = c.kv_heads;
       g.max_pos = c.max_pos; g.Q = x->q;
     } else if (which == 1) {
-      g.W = l.wo; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act; g.rpw = x->rpw_o;
+      g.W = l.wo; g.wscale = l.so; g.wdtype = c.wdtype; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act; g.rpw = x->rpw_o;
     } else if (which == 2) {
-      g.W = l.wgu; g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
+      g.W = l.wgu; g.wscale = l.sgu; g.wdtype = c.wdtype; g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
       g.rpw = x->rpw_gu;
     } else {
-      g.W = l.wd; g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
+      g.W = l.wd; g.wscale = l.sd; g.wdtype = c.wdtype; g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
     }
     g.xstride = g.K; g.ystride = g.N;
     return g;
@@ -754,7 +798,7 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int reps, float* us_out,
   (void)hipGraphDestroy(g);
   *us_out = 1e3f * ms / (reps * c.layers);
   const GemvArgs a0 = args(0);
-  if (bytes_out) *bytes_out = 2.0 * a0.N * a0.K;
+  if (bytes_out) *bytes_out = (double)x->esz * a0.N * a0.K + (x->esz == 1 ? 4.0 * a0.N : 0.0);
   return MX_OK;
 }
 

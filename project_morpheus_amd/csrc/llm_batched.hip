@@ -61,6 +61,10 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] * scale[nt];
+      if (a.wdtype == WT_FP8) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] *= a.wscale[min(nb + i, a.N - 1)];
+      }
       if (!bok || nb >= a.N) continue;
       if (EPI == EPI_STORE) {
 #pragma unroll
@@ -152,7 +156,11 @@ __device__ __forceinline__ float ld_wt(const float* p) {
 // K ranges (gridDim.y of them) give the grid its parallelism; each publishes its partial
 // tiles with write-through (sc1) stores, and the last arriving range sums them in range
 // order (deterministic) and runs the epilogue (MI355X_MICROARCH.md "Valid forms", row 1).
-template <int MT, int NT, int EPI, bool NORM, int SUB>
+// F8: weights are OCP e4m3 (16 per 16-byte load = two MFMA k-steps; converted to bf16 in
+// registers by v_cvt_scalef32_pk_bf16_fp8, exact) with a per-row scale in the epilogue.  A
+// lane's 16 bytes hold k = 64 P + 16 g .. +15, so k-step 2P + h contracts k = 64 P + 16 g +
+// 8 h + j, and the activation fragments are staged in that (consistent) k order.
+template <int MT, int NT, int EPI, bool NORM, int SUB, bool F8>
 __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
   constexpr int NP = 3, ST = 4;             // activation parts; k-steps per sub-chunk
   constexpr int ITEMS = (NT * 16 * 16) / 512 > 0 ? (NT * 16 * 16) / 512 : 1;  // X pieces/thread
@@ -183,14 +191,16 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int n = min(n0 + 16 * mt + c, a.N - 1);
-    wrow[mt] = reinterpret_cast<const uint4*>(a.W + (size_t)n * a.K) + g;
+    wrow[mt] = F8 ? reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(a.W) + (size_t)n * a.K) + g
+                  : reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.W) + (size_t)n * a.K) + g;
   }
   float ssp[ITEMS];
 #pragma unroll
   for (int it = 0; it < ITEMS; ++it) ssp[it] = 0.f;
 
   float4 xr[2][ITEMS][2], nr[2][ITEMS][2];
-  uint4 wv[2][ST][MT];
+  constexpr int WL = F8 ? ST / 2 : ST;      // 16-byte weight loads per row per sub-chunk
+  uint4 wv[2][WL][MT];
   auto load_x = [&](int sub, int buf) {
     const int k = kr0 + 128 * sub;
 #pragma unroll
@@ -205,11 +215,25 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
     }
   };
   auto load_w = [&](int sub, int buf) {
-    const int k8 = (kr0 + 128 * sub) >> 3;
+    const int kq = (kr0 + 128 * sub) / (F8 ? 16 : 8);  // in 16-byte units of a row
 #pragma unroll
-    for (int st = 0; st < ST; ++st)
+    for (int l = 0; l < WL; ++l)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) wv[buf][st][mt] = load_nt(wrow[mt] + k8 + 4 * st);
+      for (int mt = 0; mt < MT; ++mt) wv[buf][l][mt] = load_nt(wrow[mt] + kq + 4 * l);
+  };
+  // A fragment of k-step st for weight tile mt
+  auto afrag = [&](int buf, int st, int mt) -> bf16x8 {
+    if (!F8) return __builtin_bit_cast(bf16x8, wv[buf][st][mt]);
+    const uint4 q = wv[buf][st >> 1][mt];
+    const uint32_t d0 = (st & 1) ? q.z : q.x, d1 = (st & 1) ? q.w : q.y;
+    const bf16x2_t e0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, false);
+    const bf16x2_t e1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, true);
+    const bf16x2_t e2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, false);
+    const bf16x2_t e3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, true);
+    return __builtin_bit_cast(bf16x8, make_uint4(__builtin_bit_cast(uint32_t, e0),
+                                                 __builtin_bit_cast(uint32_t, e1),
+                                                 __builtin_bit_cast(uint32_t, e2),
+                                                 __builtin_bit_cast(uint32_t, e3)));
   };
   auto stage_x = [&](int buf) {
     if (!xact) return;
@@ -227,10 +251,12 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
       }
       bf16x8 pf[NP];
       split_parts<NP>(x, pf);
-      const int b = xb[it], j = xj[it];
+      const int b = xb[it], j = xj[it];  // 8 activations at k = 8 j of the sub-chunk
+      const int st = F8 ? 2 * (j >> 3) + (j & 1) : j >> 2;
+      const int gq = F8 ? (j & 7) >> 1 : j & 3;
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        xs[buf][p][b >> 4][j >> 2][(j & 3) * 16 + (b & 15)] = __builtin_bit_cast(uint4, pf[p]);
+        xs[buf][p][b >> 4][st][gq * 16 + (b & 15)] = __builtin_bit_cast(uint4, pf[p]);
     }
   };
 
@@ -260,8 +286,8 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
           const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xs[cur][p][nt][st][lane]);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, wv[cur][st][mt]), xb8, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(cur, st, mt), xb8,
+                                                                  acc[mt][nt], 0, 0, 0);
         }
       }
     }
@@ -350,6 +376,7 @@ static int rows_nkc(int N, int K, int R, int MT, int NT) {
 
 template <int MT, int NT, int EPI, bool NORM, int SUB>
 static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
+  if (a.wdtype == WT_FP8 && a.K % 128) return hipErrorNotSupported;
   const int tiles_n = (a.N + 128 * MT - 1) / (128 * MT), tiles_r = (a.R + 16 * NT - 1) / (16 * NT);
   if (nkc > 1) {
     const size_t need = (size_t)tiles_n * tiles_r * nkc * (8 * MT * NT * 4 * 64 + 16 * NT);
@@ -357,7 +384,10 @@ static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
       return hipErrorInvalidValue;
   }
   const dim3 grid(tiles_n, nkc, tiles_r);
-  hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB>), grid, dim3(512), 0, st, a);
+  if (a.wdtype == WT_FP8)
+    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, true>), grid, dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, false>), grid, dim3(512), 0, st, a);
   return hipGetLastError();
 }
 

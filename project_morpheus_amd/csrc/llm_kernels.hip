@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int n = min(n0 + i, a.N - 1);  // tail rows (lm_head) re-read the last row
-      wp[i] = reinterpret_cast<const uint4*>(a.W + (size_t)n * a.K);
+      wp[i] = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.W) + (size_t)n * a.K);
     }
 #pragma unroll 4
     for (int c = lane; c < K8; c += 64) {
@@ -212,12 +212,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
 //   Epilogue operands that do not depend on the result (residual, RoPE row) are fetched
 //   with the activation.
 // ---------------------------------------------------------------------------------
-template <int KCH, int RPW, int EPI, bool NORM, int WPB>
+// F8: weights are OCP e4m3 bytes with one fp32 scale per row (16 weights per 16-byte load,
+// converted in registers by v_cvt_pk_f32_fp8 -- exact), else bf16 (8 per load).
+template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8>
 __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   constexpr int NT = WPB * 64;
-  constexpr int K8 = KCH * 64;                 // 16-byte weight chunks per row
-  constexpr int XPT = (K8 + NT - 1) / NT;      // activation chunks per thread
-  __shared__ __attribute__((aligned(16))) float4 xs[2 * K8];  // lo plane | hi plane
+  constexpr int EPC = F8 ? 16 : 8;             // weights per 16-byte chunk
+  constexpr int PL = EPC / 4;                  // float4 planes of the staged activation
+  constexpr int KC = KCH * 64;                 // 16-byte weight chunks per row
+  constexpr int XPT = (KC + NT - 1) / NT;      // activation chunks per thread
+  __shared__ __attribute__((aligned(16))) float4 xs[PL * KC];  // plane q at [q * KC + m]
   __shared__ float red[WPB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = a.N / RPW;
@@ -229,29 +233,32 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   // 1. activation (+ norm weight, + epilogue operands)
   const float4* X4 = reinterpret_cast<const float4*>(a.X);
   const float4* NW4 = reinterpret_cast<const float4*>(a.norm_w);
-  float4 xl[XPT], xh[XPT], nl[XPT], nh[XPT];
+  float4 xv[XPT][PL], nv[XPT][PL];
 #pragma unroll
   for (int i = 0; i < XPT; ++i) {
-    const int c8 = min(tid + i * NT, K8 - 1);
-    xl[i] = X4[2 * c8];
-    xh[i] = X4[2 * c8 + 1];
-    if (NORM) {
-      nl[i] = NW4[2 * c8];
-      nh[i] = NW4[2 * c8 + 1];
+    const int m = min(tid + i * NT, KC - 1);
+#pragma unroll
+    for (int q = 0; q < PL; ++q) {
+      xv[i][q] = X4[PL * m + q];
+      if (NORM) nv[i][q] = NW4[PL * m + q];
     }
   }
-  float res[RPW];
+  float res[RPW], wsc[RPW];
   if (EPI == EPI_RESID) {
 #pragma unroll
     for (int r = 0; r < RPW; ++r) res[r] = a.Y[n0 + r];
   }
+  if (F8) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) wsc[r] = a.wscale[n0 + r];
+  }
   // 2. every weight load of this wave
   uint4 w[RPW][KCH];
-  const uint4* wp = reinterpret_cast<const uint4*>(a.W) + (size_t)n0 * K8 + lane;
+  const uint4* wp = reinterpret_cast<const uint4*>(a.W) + (size_t)n0 * KC + lane;
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
-    for (int c = 0; c < KCH; ++c) w[r][c] = load_nt(wp + (size_t)r * K8 + c * 64);
+    for (int c = 0; c < KCH; ++c) w[r][c] = load_nt(wp + (size_t)r * KC + c * 64);
   __builtin_amdgcn_sched_barrier(0);
 
   // 3. prologue under the weight latency
@@ -260,9 +267,11 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
-      if (tid + i * NT < K8) {
-        ss += xl[i].x * xl[i].x + xl[i].y * xl[i].y + xl[i].z * xl[i].z + xl[i].w * xl[i].w;
-        ss += xh[i].x * xh[i].x + xh[i].y * xh[i].y + xh[i].z * xh[i].z + xh[i].w * xh[i].w;
+      if (tid + i * NT < KC) {
+#pragma unroll
+        for (int q = 0; q < PL; ++q)
+          ss += xv[i][q].x * xv[i][q].x + xv[i][q].y * xv[i][q].y + xv[i][q].z * xv[i][q].z +
+                xv[i][q].w * xv[i][q].w;
       }
     }
     ss = wave_sum(ss);
@@ -271,21 +280,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
     float tot = 0.f;
 #pragma unroll
     for (int i = 0; i < WPB; ++i) tot += red[i];
-    scale = 1.0f / sqrtf(tot / (float)(K8 * 8) + a.eps);
+    scale = 1.0f / sqrtf(tot / (float)(KC * EPC) + a.eps);
   }
 #pragma unroll
   for (int i = 0; i < XPT; ++i) {
-    const int c8 = tid + i * NT;
-    if (c8 < K8) {
-      float4 lo = xl[i], hi = xh[i];
-      if (NORM) {
-        lo.x = lo.x * scale * nl[i].x; lo.y = lo.y * scale * nl[i].y;
-        lo.z = lo.z * scale * nl[i].z; lo.w = lo.w * scale * nl[i].w;
-        hi.x = hi.x * scale * nh[i].x; hi.y = hi.y * scale * nh[i].y;
-        hi.z = hi.z * scale * nh[i].z; hi.w = hi.w * scale * nh[i].w;
+    const int m = tid + i * NT;
+    if (m < KC) {
+#pragma unroll
+      for (int q = 0; q < PL; ++q) {
+        float4 v = xv[i][q];
+        if (NORM) {
+          v.x = v.x * scale * nv[i][q].x; v.y = v.y * scale * nv[i][q].y;
+          v.z = v.z * scale * nv[i][q].z; v.w = v.w * scale * nv[i][q].w;
+        }
+        xs[q * KC + m] = v;
       }
-      xs[c8] = lo;
-      xs[K8 + c8] = hi;
     }
   }
   __syncthreads();
@@ -296,12 +305,32 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   for (int r = 0; r < RPW; ++r) acc[r] = 0.f;
 #pragma unroll
   for (int c = 0; c < KCH; ++c) {
-    const float4 lo = xs[c * 64 + lane], hi = xs[K8 + c * 64 + lane];
+    float4 xq[PL];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) acc[r] = dot8(w[r][c], lo, hi, acc[r]);
+    for (int q = 0; q < PL; ++q) xq[q] = xs[q * KC + c * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      if (F8) {
+        const uint32_t wd[4] = {w[r][c].x, w[r][c].y, w[r][c].z, w[r][c].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
+          const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
+          acc[r] = fmaf(lo.x, xq[q].x, acc[r]);
+          acc[r] = fmaf(lo.y, xq[q].y, acc[r]);
+          acc[r] = fmaf(hi.x, xq[q].z, acc[r]);
+          acc[r] = fmaf(hi.y, xq[q].w, acc[r]);
+        }
+      } else {
+        acc[r] = dot8(w[r][c], xq[0], xq[1], acc[r]);
+      }
+    }
   }
 #pragma unroll
-  for (int r = 0; r < RPW; ++r) acc[r] = wave_sum(acc[r]);
+  for (int r = 0; r < RPW; ++r) {
+    acc[r] = wave_sum(acc[r]);
+    if (F8) acc[r] *= wsc[r];
+  }
   if (!active || lane != 0) return;
 
   // 5. epilogues
@@ -660,17 +689,20 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(const int32_t* ids, int
   }
 }
 
-// Row permutation copy used to pack weights (dst row i <- src row perm[i]); converts
-// f32 sources to bf16 when src_f32.
-__global__ void pack_rows_kernel(uint16_t* dst, const void* src, const int32_t* perm,
-                                 int cols, int src_f32) {
+// Weight packing: source row i -> destination row dmap[i].  mode 0: bf16 -> bf16,
+// 1: f32 -> bf16 (RNE), 2: bytes (fp8 e4m3) -> bytes.
+__global__ void scatter_rows_kernel(void* dst, const void* src, const int32_t* dmap, int cols,
+                                    int mode) {
   const int i = blockIdx.x;
-  const int s = perm[i];
+  const size_t d = (size_t)dmap[i] * cols, s = (size_t)i * cols;
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
-    uint16_t v;
-    if (src_f32) v = f32_to_bf16(reinterpret_cast<const float*>(src)[(size_t)s * cols + c]);
-    else v = reinterpret_cast<const uint16_t*>(src)[(size_t)s * cols + c];
-    dst[(size_t)i * cols + c] = v;
+    if (mode == 2) {
+      static_cast<uint8_t*>(dst)[d + c] = static_cast<const uint8_t*>(src)[s + c];
+    } else {
+      const uint16_t v = mode == 1 ? f32_to_bf16(static_cast<const float*>(src)[s + c])
+                                   : static_cast<const uint16_t*>(src)[s + c];
+      static_cast<uint16_t*>(dst)[d + c] = v;
+    }
   }
 }
 
@@ -721,32 +753,36 @@ static int gemv_blocks(int N, int rpw, int ytiles, int target) {
   return b < cap ? b : (cap > 0 ? cap : 1);
 }
 
-template <int KCH, int RPW, int EPI, bool NORM>
+template <int KCH, int RPW, int EPI, bool NORM, bool F8>
 static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
   const int G = a.N / RPW;
-  if (a.wpb == 4)
-    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 4>), dim3((G + 3) / 4), dim3(256), 0, st, a);
+  if (a.wpb == 8)
+    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8>), dim3((G + 7) / 8), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8>), dim3((G + 7) / 8), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 4, F8>), dim3((G + 3) / 4), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 // B = 1 path; returns hipErrorNotSupported when the shape has no instantiation.
-// a.rpw (0 = default per epilogue) picks rows per wave: QKV 2, RESID/STORE 1, SILU 4|2.
+// a.rpw (0 = default per epilogue) picks rows per wave: QKV 2, RESID/STORE 1, SILU 2.
+// KCH = 16-byte weight chunks per lane per row: K / 512 (bf16) or K / 1024 (fp8).
 static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
-  if (a.K % 512) return hipErrorNotSupported;
-  const int kch = a.K / 512;
+  const bool f8 = a.wdtype == WT_FP8;
+  const int epc = f8 ? 1024 : 512;
+  if (a.K % epc) return hipErrorNotSupported;
+  const int kch = a.K / epc;
   int rpw = a.rpw;
   if (rpw == 0) rpw = epi == EPI_QKV ? 2 : epi == EPI_SILU ? 2 : 1;
 #define MX_G1(KCH_, RPW_, EPI_, NORM_)                                                  \
   if (kch == KCH_ && rpw == RPW_ && epi == EPI_ && norm == NORM_ && a.N % RPW_ == 0)     \
-    return launch_gemv1_t<KCH_, RPW_, EPI_, NORM_>(a, st);
+    return f8 ? launch_gemv1_t<KCH_, RPW_, EPI_, NORM_, true>(a, st)                    \
+              : launch_gemv1_t<KCH_, RPW_, EPI_, NORM_, false>(a, st);
 #define MX_G1K(KCH_)                                                                     \
   MX_G1(KCH_, 2, EPI_QKV, true) MX_G1(KCH_, 1, EPI_RESID, false)                       \
   MX_G1(KCH_, 2, EPI_RESID, false)                                                      \
   MX_G1(KCH_, 2, EPI_SILU, true) MX_G1(KCH_, 4, EPI_SILU, true)                         \
   MX_G1(KCH_, 1, EPI_STORE, false) MX_G1(KCH_, 1, EPI_STORE, true)
-  MX_G1K(1) MX_G1K(2) MX_G1K(4) MX_G1K(6) MX_G1K(8) MX_G1K(16)
+  MX_G1K(1) MX_G1K(2) MX_G1K(3) MX_G1K(4) MX_G1K(6) MX_G1K(8) MX_G1K(16)
 #undef MX_G1K
 #undef MX_G1
   return hipErrorNotSupported;
@@ -757,9 +793,10 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported) return e;
   }
-  if (a.R >= 2 && !a.force_legacy) {
+  // multi-row steps, and the fp8 single-row lm_head, run on the MFMA kernel
+  if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
     const hipError_t e = launch_gemm_rows(a, epi, norm, st);
-    if (e != hipErrorNotSupported) return e;
+    if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
   }
   // RT = 1 for the decode batch of 1; RT = 4 otherwise (prefill / batched decode).
   const int RT = a.R == 1 ? 1 : 4;
@@ -832,9 +869,9 @@ hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t
   return hipGetLastError();
 }
 
-hipError_t launch_pack_rows(uint16_t* dst, const void* src, const int32_t* perm, int rows,
-                            int cols, int src_f32, hipStream_t st) {
-  hipLaunchKernelGGL(pack_rows_kernel, dim3(rows), dim3(256), 0, st, dst, src, perm, cols, src_f32);
+hipError_t launch_scatter_rows(void* dst, const void* src, const int32_t* dmap, int rows,
+                               int cols, int mode, hipStream_t st) {
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(rows), dim3(256), 0, st, dst, src, dmap, cols, mode);
   return hipGetLastError();
 }
 

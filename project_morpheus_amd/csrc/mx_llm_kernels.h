@@ -6,6 +6,7 @@
 namespace mx {
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_QKV = 3, EPI_ARGMAX = 4 };
+enum { WT_BF16 = 0, WT_FP8 = 1 };  // weight storage: bf16, or OCP e4m3 + fp32 scale per row
 
 constexpr int ATT_S_MIN = 128;      // smallest split (positions) = 4 waves x 32
 constexpr int ATT_MAX_SPLITS = 256; // splits one launch may merge
@@ -13,7 +14,9 @@ constexpr int ATT_MAXG = 4;         // max q-heads per kv-head
 constexpr int ATT_MERGE_CHUNK = 16; // splits whose partials the merging block prefetches
 
 struct GemvArgs {
-  const uint16_t* W;       // [N][K] bf16, packed row order
+  const void* W;           // [N][K] bf16 (WT_BF16) or e4m3 bytes (WT_FP8), packed row order
+  const float* wscale;     // WT_FP8: dequant scale per row [N]
+  int wdtype;
   int N, K;
   const float* X;          // activations, row r at X + r * xstride
   int xstride;
@@ -91,8 +94,8 @@ hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t s
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st);
 hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t* embed,
                              int hidden, int vocab, uint8_t* seen, float* h, hipStream_t st);
-hipError_t launch_pack_rows(uint16_t* dst, const void* src, const int32_t* perm, int rows,
-                            int cols, int src_f32, hipStream_t st);
+hipError_t launch_scatter_rows(void* dst, const void* src, const int32_t* dmap, int rows,
+                               int cols, int mode, hipStream_t st);
 hipError_t launch_to_f32(float* dst, const void* src, int64_t n, int src_bf16, hipStream_t st);
 
 }  // namespace mx

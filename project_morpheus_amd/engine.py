@@ -34,6 +34,8 @@ def _dtype_code(t: torch.Tensor) -> int:
         return _lib.MX_DTYPE_BF16
     if t.dtype == torch.float32:
         return _lib.MX_DTYPE_F32
+    if t.dtype == torch.float8_e4m3fn:
+        return _lib.MX_DTYPE_FP8
     raise TypeError(f"unsupported weight dtype {t.dtype}")
 
 
@@ -42,7 +44,8 @@ class LlmEngine:
 
     def __init__(self, cfg: OrpheusConfig, weights: Dict[str, torch.Tensor], device: int = 0,
                  max_slots: int = 4, max_pos: int = 2048, max_batch: int = 1,
-                 max_prefill: int = 256):
+                 max_prefill: int = 256, wdtype: str = "bf16"):
+        """``wdtype="fp8"``: matrices as e4m3 + per-row ``.scale`` (weights.quantize_fp8)."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.cfg, self.device = cfg, device
@@ -52,7 +55,8 @@ class LlmEngine:
                            kv_heads=cfg.kv_heads, head_dim=cfg.head_dim, ffn=cfg.ffn,
                            vocab=cfg.vocab, max_slots=max_slots, max_pos=max_pos,
                            max_batch=max_batch, max_prefill=max_prefill, eps=cfg.eps,
-                           tied=int(cfg.tied))
+                           tied=int(cfg.tied), wdtype=_lib.MX_WEIGHTS[wdtype])
+        self.wdtype = wdtype
         h = C.c_void_p()
         torch.cuda.set_device(device)
         rc = self.lib.mx_llm_create(device, C.byref(c), C.byref(h))

@@ -84,6 +84,46 @@ def load_hf_llm(path: str, device="cpu") -> Dict[str, torch.Tensor]:
     return out
 
 
+def quantize_fp8(weights: Dict[str, torch.Tensor], cfg: OrpheusConfig) -> Dict[str, torch.Tensor]:
+    """bf16/f32 Orpheus weights -> the fp8 engine's inputs (BASELINE configs[4]).
+
+    Every matrix but the token embedding becomes OCP e4m3 (``torch.float8_e4m3fn``) with one
+    fp32 scale per output row, ``scale = max|W_row| / 448`` (448 = e4m3 max), ``q = W /
+    scale`` rounded to nearest-even; ``"<name>.scale"`` carries the scales.  A tied lm_head
+    is materialised as its own fp8 matrix (the bf16 embedding stays for the token lookup).
+    The dequantised model (``dequantize_fp8``) is what the fp8 parity oracle runs.
+    """
+    out = {}
+    mats = [k for k, v in weights.items() if v.dim() == 2 and k != "embed"]
+    src = dict(weights)
+    if "lm_head" not in src:
+        src["lm_head"] = weights["embed"]
+        mats.append("lm_head")
+    for k, v in weights.items():
+        if k not in mats:
+            out[k] = v
+    for k in mats:
+        w = src[k].float()
+        amax = w.abs().amax(dim=1)
+        scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        out[k] = (w / scale[:, None]).to(torch.float8_e4m3fn)
+        out[k + ".scale"] = scale.float().contiguous()
+    return out
+
+
+def dequantize_fp8(qw: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """fp8 engine inputs -> fp32 weights for the CPU oracle: W = scale[row] * e4m3."""
+    out = {}
+    for k, v in qw.items():
+        if k.endswith(".scale"):
+            continue
+        if v.dtype == torch.float8_e4m3fn:
+            out[k] = v.float() * qw[k + ".scale"][:, None]
+        else:
+            out[k] = v
+    return out
+
+
 # ------------------------------------------------------------------------------------ SNAC
 def snac_shapes() -> Dict[str, tuple]:
     s = {}

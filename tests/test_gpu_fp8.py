@@ -1,0 +1,82 @@
+"""fp8 (OCP e4m3, per-row scales) decode vs the CPU oracle run on the dequantised weights.
+
+BASELINE configs[4].  The oracle (oracle/llama_ref.py) runs exactly the model the GPU runs:
+W = scale[row] * e4m3 (weights.dequantize_fp8).  Single-row steps use the fp8 GEMV
+(v_cvt_pk_f32_fp8), the lm_head and multi-row steps the fp8 -> bf16 MFMA kernel.
+Tolerances as tests/test_gpu_llm.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import llama_ref as L
+from project_morpheus_amd import config as C
+from project_morpheus_amd.weights import (dequantize_fp8, quantize_fp8,
+                                          synthetic_llm_weights)
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 5e-3
+TIE_MARGIN = 1e-2
+
+
+def _cfg():
+    return C.OrpheusConfig(hidden=1024, layers=2, heads=8, kv_heads=2, ffn=2048, vocab=1000)
+
+
+def _run(cfg, qw, prompts, steps):
+    from project_morpheus_amd.engine import LlmEngine
+    B = len(prompts)
+    eng = LlmEngine(cfg, qw, device=0, max_slots=B, max_pos=512, max_batch=B, max_prefill=128,
+                    wdtype="fp8")
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    toks = [[] for _ in range(B)]
+    logits = [[] for _ in range(B)]
+    for r, p in enumerate(prompts):
+        eng.prefill(r, r, p, 1.1, st)
+    for k in range(steps):
+        if k > 0:
+            eng.decode(B, 1.1, st)
+        st.synchronize()
+        for r, p in enumerate(prompts):
+            logits[r].append(eng.read_logits(r, st))
+            toks[r].append(int(eng.hist[r, len(p) + k]))
+    eng.close()
+    return toks, logits
+
+
+def _check(cfg, qw, prompts, steps):
+    toks, logits = _run(cfg, qw, prompts, steps)
+    rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                     kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
+    ref = L.LlamaRef(rc, dequantize_fp8(qw), max_pos=512)
+    agree = 0
+    for r, p in enumerate(prompts):
+        _, rl = L.greedy_generate(ref, p, steps, 1.1, return_logits=True, forced=toks[r])
+        for k in range(steps):
+            o = rl[k].numpy()
+            np.testing.assert_allclose(logits[r][k], o, atol=LOGIT_TOL, rtol=LOGIT_TOL,
+                                       err_msg=f"row {r} step {k}")
+            if toks[r][k] != int(np.argmax(o)):
+                top2 = np.sort(o)[-2:]
+                assert top2[1] - top2[0] < TIE_MARGIN
+            else:
+                agree += 1
+    return agree
+
+
+def test_fp8_single_stream():
+    cfg = _cfg()
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=51, std=0.05, norm_jitter=0.5), cfg)
+    rng = np.random.default_rng(12)
+    prompt = [int(x) for x in rng.integers(0, cfg.vocab, 17)]
+    assert _check(cfg, qw, [prompt], 30) >= 24
+
+
+def test_fp8_batched_6_rows():
+    cfg = _cfg()
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=52, std=0.05, norm_jitter=0.5), cfg)
+    rng = np.random.default_rng(13)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 4 + 3 * i)] for i in range(6)]
+    assert _check(cfg, qw, prompts, 10) >= 0.8 * 60
