@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--profile-steps", type=int, default=24)
     p.add_argument("--batch", type=int, default=32,
                    help="configs[2]: concurrent streams per GPU (0 skips it)")
+    p.add_argument("--fp8-batch", type=int, default=8,
+                   help="configs[4]: fp8 streams per GPU (0 skips the fp8 section)")
     p.add_argument("--step-pos", type=int, default=600,
                    help="position at which the bare decode-step time is measured")
     return p.parse_args()
@@ -95,10 +97,12 @@ def cpu_baseline(cfg, prompt, n_decode=6):
             "tok_per_s": round(1.0 / t_tok, 3)}
 
 
-def run_batched(args, llm, snac, prompt, rank, world, dist):
-    """configs[2]: ``args.batch`` utterances per GPU arriving with exponential gaps (mean
-    10 ms, seed 4), synthetic prompts of 16-64 ids, ``max_tokens`` each, served by the
-    continuous-batching loop; aggregate RTF = all audio / wall time (max over ranks)."""
+def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, label=None):
+    """configs[2]: ``n_streams`` (default ``args.batch``) utterances per GPU arriving with
+    exponential gaps (mean 10 ms, seed 4), synthetic prompts of 16-64 ids, ``max_tokens``
+    each, served by the continuous-batching loop; aggregate RTF = all audio / wall time
+    (max over ranks)."""
+    n_streams = n_streams or args.batch
     import numpy as np
     import torch
 
@@ -109,7 +113,7 @@ def run_batched(args, llm, snac, prompt, rank, world, dist):
 
     def requests():
         t, out = 0.0, []
-        for i in range(args.batch):
+        for i in range(n_streams):
             n = int(rng.integers(16, 65))
             ids = I.prompt_ids([int(x) for x in rng.integers(1000, 120000, n - 5)])
             out.append(StreamRequest(prompt_ids=ids, max_tokens=args.max_tokens, arrival=t,
@@ -137,13 +141,54 @@ def run_batched(args, llm, snac, prompt, rank, world, dist):
         fl = [None] * world
         dist.all_gather_object(fl, firsts)
         firsts = [x for r in fl for x in r]
-    return {"workload": f"configs[2]: {args.batch} concurrent utterances per GPU, "
-                        "continuous batching, batched SNAC, exp arrivals mean 10 ms (seed 4)",
-            "streams": args.batch * world, "value": round(audio / wall, 3),
+    return {"workload": label or (f"configs[2]: {n_streams} concurrent utterances per GPU, "
+                                  "continuous batching, batched SNAC, exp arrivals mean 10 ms "
+                                  "(seed 4)"),
+            "streams": n_streams * world, "value": round(audio / wall, 3),
             "unit": "audio-sec/wall-sec", "wall_s": round(wall, 3),
             "audio_seconds": round(audio, 2),
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
-            "tok_per_s": round(args.batch * world * args.max_tokens / wall, 1)}
+            "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
+
+
+def run_fp8(args, cfg, local, snac, prompt, inject, rank, world, dist):
+    """configs[4] on this GPU: Orpheus-3B with fp8 e4m3 weights (per-row scales), fp8
+    GEMV / fp8->bf16 MFMA kernels; ``args.fp8_batch`` streams per GPU batched, plus one
+    single-stream utterance (the north_star's >= 30x single-stream target)."""
+    import torch
+
+    from project_morpheus_amd.engine import LlmEngine, Synthesizer, UtteranceStats
+    from project_morpheus_amd.weights import quantize_fp8, synthetic_llm_weights
+    w = quantize_fp8(synthetic_llm_weights(cfg, seed=0, device=f"cuda:{local}"), cfg)
+    llm8 = LlmEngine(cfg, w, device=local, max_slots=args.fp8_batch, max_pos=2048,
+                     max_batch=args.fp8_batch, max_prefill=256, wdtype="fp8")
+    del w
+    torch.cuda.empty_cache()
+    out = {"weights": "fp8 e4m3 + fp32 per-row scale (3.30 GB streamed per step)"}
+    out["batched"] = run_batched(args, llm8, snac, prompt, rank, world, dist,
+                                 n_streams=args.fp8_batch,
+                                 label=f"configs[4]: fp8, {args.fp8_batch} streams per GPU "
+                                       f"({args.fp8_batch * 8} over 8 GPUs), continuous "
+                                       "batching, batched SNAC")
+    syn = Synthesizer(llm8, snac, depth=3, seed=rank)
+
+    def utt():
+        st = UtteranceStats()
+        for _ in syn.run(prompt, args.max_tokens, 1.1, stop_ids=(), inject_ids=inject, stats=st):
+            pass
+        return st
+    utt()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = utt()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    out["single_stream"] = {"value": round(st.audio_seconds / wall, 3),
+                            "unit": "audio-sec/wall-sec",
+                            "first_audio_ms": round(st.first_audio_ms, 2),
+                            "ms_per_token": round(1e3 * wall / st.tokens, 4)}
+    llm8.close()
+    return out
 
 
 def main():
@@ -215,6 +260,11 @@ def main():
     if B3 > 0:
         batched = run_batched(args, llm, snac, prompt, rank, world, dist)
 
+    # ---- configs[4] per GPU: fp8 weights, args.fp8_batch streams per GPU (64 over 8 GPUs) ----
+    fp8 = None
+    if args.fp8_batch > 0:
+        fp8 = run_fp8(args, cfg, local, snac, prompt, inject, rank, world, dist)
+
     # ---- roofline of the dominant kernel (gate/up GEMV, 2*ffn*hidden bf16 per launch) ----
     # HIP events around one hipGraph of back-to-back launches of that kernel sweeping all 28
     # layers' weights (as a decode step streams them), on the engine's capture stream
@@ -270,6 +320,7 @@ def main():
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
             "audio_seconds": round(audio, 3),
             "configs_2_batched": batched,
+            "configs_4_fp8": fp8,
             "decode_step_ms": round(step_ms, 4),
             "decode_tok_per_s": round(1e3 / step_ms, 1),
             "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),

@@ -20,7 +20,7 @@ namespace mx {
 // Grid: x = row-group workers (grid-stride over N / RPW groups, one wave per group),
 //       y = ceil(R / RT) activation-row tiles.
 // ---------------------------------------------------------------------------------
-template <int RT, int RPW, int EPI, bool NORM>
+template <int RT, int RPW, int EPI, bool NORM, bool F8 = false>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K8 = a.K >> 3;
@@ -94,24 +94,56 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int n = min(n0 + i, a.N - 1);  // tail rows (lm_head) re-read the last row
-      wp[i] = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.W) + (size_t)n * a.K);
+      wp[i] = F8 ? reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(a.W) + (size_t)n * a.K)
+                 : reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.W) + (size_t)n * a.K);
     }
+    if (F8) {  // 16 e4m3 weights per 16-byte chunk = activation chunks 2c, 2c+1
 #pragma unroll 4
-    for (int c = lane; c < K8; c += 64) {
-      uint4 w[RPW];
+      for (int c = lane; c < (K8 >> 1); c += 64) {
+        uint4 w[RPW];
 #pragma unroll
-      for (int i = 0; i < RPW; ++i) w[i] = load_nt(wp[i] + c);
+        for (int i = 0; i < RPW; ++i) w[i] = load_nt(wp[i] + c);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const float4 lo = xlo[rt * K8 + c], hi = xhi[rt * K8 + c];
+        for (int rt = 0; rt < RT; ++rt) {
+          const float4 x0 = xlo[rt * K8 + 2 * c], x1 = xhi[rt * K8 + 2 * c];
+          const float4 x2 = xlo[rt * K8 + 2 * c + 1], x3 = xhi[rt * K8 + 2 * c + 1];
 #pragma unroll
-        for (int i = 0; i < RPW; ++i) acc[i][rt] = dot8(w[i], lo, hi, acc[i][rt]);
+          for (int i = 0; i < RPW; ++i) {
+            const uint32_t wd[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
+            const float4 xx[4] = {x0, x1, x2, x3};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
+              const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
+              acc[i][rt] = fmaf(lo.x, xx[q].x, acc[i][rt]);
+              acc[i][rt] = fmaf(lo.y, xx[q].y, acc[i][rt]);
+              acc[i][rt] = fmaf(hi.x, xx[q].z, acc[i][rt]);
+              acc[i][rt] = fmaf(hi.y, xx[q].w, acc[i][rt]);
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll 4
+      for (int c = lane; c < K8; c += 64) {
+        uint4 w[RPW];
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) w[i] = load_nt(wp[i] + c);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const float4 lo = xlo[rt * K8 + c], hi = xhi[rt * K8 + c];
+#pragma unroll
+          for (int i = 0; i < RPW; ++i) acc[i][rt] = dot8(w[i], lo, hi, acc[i][rt]);
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[i][rt] = wave_sum(acc[i][rt]);
+      for (int rt = 0; rt < RT; ++rt) {
+        acc[i][rt] = wave_sum(acc[i][rt]);
+        if (F8) acc[i][rt] *= a.wscale[min(n0 + i, a.N - 1)];
+      }
 
     // ---- epilogues (every lane holds every total; lane 0 writes) -----------------------
     if (EPI == EPI_ARGMAX) {
@@ -737,12 +769,12 @@ __global__ void to_f32_kernel(float* dst, const void* src, int64_t n, int src_bf
 // ---------------------------------------------------------------------------------
 // Host-side launchers
 // ---------------------------------------------------------------------------------
-template <int RT, int RPW, int EPI, bool NORM>
+template <int RT, int RPW, int EPI, bool NORM, bool F8 = false>
 static hipError_t launch_gemv_t(const GemvArgs& a, int blocks, hipStream_t st) {
   const size_t lds = (size_t)RT * a.K * 4 + 64;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int ytiles = (a.R + RT - 1) / RT;
-  hipLaunchKernelGGL((gemv_kernel<RT, RPW, EPI, NORM>), dim3(blocks, ytiles), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemv_kernel<RT, RPW, EPI, NORM, F8>), dim3(blocks, ytiles), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
@@ -793,7 +825,12 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported) return e;
   }
-  // multi-row steps, and the fp8 single-row lm_head, run on the MFMA kernel
+  // fp8 single-row lm_head: the grid-stride argmax GEMV with e4m3 weights
+  if (a.R == 1 && epi == EPI_ARGMAX && norm && a.wdtype == WT_FP8 && a.K % 1024 == 0) {
+    const int blocks = gemv_blocks(a.N, 4, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
+    return launch_gemv_t<1, 4, EPI_ARGMAX, true, true>(a, blocks, st);
+  }
+  // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
     const hipError_t e = launch_gemm_rows(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
@@ -837,6 +874,9 @@ hipError_t gemv_prepare(int kmax) {
   MX_A(4, 2, EPI_RESID, false) MX_A(4, 2, EPI_SILU, true)
   MX_A(4, 2, EPI_QKV, true) MX_A(4, 4, EPI_ARGMAX, true)
 #undef MX_A
+  if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 4, EPI_ARGMAX, true, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
   return e;
 }
 

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--rows", type=int, default=1)
+    ap.add_argument("--fp8", action="store_true")
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -43,8 +44,12 @@ def main():
     from project_morpheus_amd.weights import synthetic_llm_weights
     cfg = C.OrpheusConfig()
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
+    if args.fp8:
+        from project_morpheus_amd.weights import quantize_fp8
+        w = quantize_fp8(w, cfg)
     R = args.rows
-    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=256)
+    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=256,
+                    wdtype="fp8" if args.fp8 else "bf16")
     del w
     torch.cuda.empty_cache()
     st = torch.cuda.Stream()
