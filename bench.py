@@ -41,6 +41,8 @@ def parse():
                    help="configs[2]: concurrent streams per GPU (0 skips it)")
     p.add_argument("--fp8-batch", type=int, default=8,
                    help="configs[4]: fp8 streams per GPU (0 skips the fp8 section)")
+    p.add_argument("--long-read-docs", type=int, default=16,
+                   help="configs[3]: long_read documents (0 skips it)")
     p.add_argument("--step-pos", type=int, default=600,
                    help="position at which the bare decode-step time is measured")
     return p.parse_args()
@@ -151,6 +153,59 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
             "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
 
 
+def run_long_read(args, llm, snac, rank, world, dist):
+    """configs[3]: ``long_read`` — 16 synthetic documents x ~3,000 chars (seed 5) split into
+    the reference's <=1000-char long-form batches, every batch an independent utterance of
+    ``max_tokens``; the jobs are sharded over the ranks (longest first, least loaded), each
+    rank serves its share through the continuous-batching loop, PCM is gathered to rank 0
+    over RCCL and stitched per document (50 ms crossfade, stitch_wav_files).  Total work is
+    fixed, so this is ``strong`` scaling; value = all documents' audio / max-over-ranks wall."""
+    import numpy as np
+    import torch
+
+    from project_morpheus_amd import sharding as S
+    from project_morpheus_amd.batching import BatchSynthesizer, StreamRequest
+    from project_morpheus_amd.tokenizer import Tokenizer
+    docs = S.long_read_documents(args.long_read_docs, 3000, seed=5)
+    jobs = S.plan_jobs(docs, Tokenizer(None).encode, "tara", args.max_tokens)
+    syn = BatchSynthesizer(llm, snac, depth=2, seed=rank)
+    job_index = {id(j): i for i, j in enumerate(jobs)}
+
+    def synthesize(mine):
+        reqs = [StreamRequest(prompt_ids=j.prompt_ids, max_tokens=j.max_tokens,
+                              inject_ids=synthetic_audio_ids(j.max_tokens,
+                                                             seed=100 + job_index[id(j)]),
+                              stop_ids=()) for j in mine]
+        syn.run(reqs, on_chunk=lambda req, data: req.pcm.append(data))
+        return [b"".join(r.pcm) for r in reqs]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = S.run_sharded(jobs, rank, world, synthesize, device="cuda" if world > 1 else None,
+                        crossfade_ms=50.0)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    if rank != 0:
+        return None
+    audio = sum(len(v) for v in out.values()) / 24000.0
+    mine = S.assign(jobs, world)
+    return {"workload": (f"configs[3]: long_read, {len(docs)} documents x ~3000 chars (seed 5) "
+                         f"-> {len(jobs)} <=1000-char batches x {args.max_tokens} tokens, "
+                         f"sharded over {world} GPU(s), continuous batching per GPU, ordered "
+                         "gather to rank 0 + 50 ms crossfade stitch"),
+            "scaling": "strong", "documents": len(docs), "jobs": len(jobs),
+            "jobs_per_rank": [len(m) for m in mine],
+            "value": round(audio / wall, 3), "unit": "audio-sec/wall-sec",
+            "wall_s": round(wall, 3), "audio_seconds": round(audio, 2),
+            "doc_samples_min": int(min(len(v) for v in out.values()))}
+
+
 def run_fp8(args, cfg, local, snac, prompt, inject, rank, world, dist):
     """configs[4] on this GPU: Orpheus-3B with fp8 e4m3 weights (per-row scales), fp8
     GEMV / fp8->bf16 MFMA kernels; ``args.fp8_batch`` streams per GPU batched, plus one
@@ -216,7 +271,7 @@ def main():
     w = synthetic_llm_weights(cfg, seed=0, device=f"cuda:{local}")
     B3 = args.batch
     llm = LlmEngine(cfg, w, device=local, max_slots=max(1, B3), max_pos=2048,
-                    max_batch=max(1, B3), max_prefill=256)
+                    max_batch=max(1, B3), max_prefill=512)
     del w
     torch.cuda.empty_cache()
     snac = SnacDecoder(synthetic_snac_weights(), device=local, max_frames=7,
@@ -259,6 +314,11 @@ def main():
     batched = None
     if B3 > 0:
         batched = run_batched(args, llm, snac, prompt, rank, world, dist)
+
+    # ---- configs[3]: long_read documents sharded over the ranks, gathered + stitched ----
+    long_read = None
+    if args.long_read_docs > 0:
+        long_read = run_long_read(args, llm, snac, rank, world, dist)
 
     # ---- configs[4] per GPU: fp8 weights, args.fp8_batch streams per GPU (64 over 8 GPUs) ----
     fp8 = None
@@ -320,6 +380,7 @@ def main():
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
             "audio_seconds": round(audio, 3),
             "configs_2_batched": batched,
+            "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,
             "decode_step_ms": round(step_ms, 4),
             "decode_tok_per_s": round(1e3 / step_ms, 1),
