@@ -89,11 +89,13 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, float penalty, void* stream,
  * "att_cpw_batch"; see capi.hip).  Drops the
  * captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
-/* Roofline probe: mean microseconds per launch of the single-row GEMV `which` (0 qkv,
- * 1 o-proj, 2 gate/up, 3 down), timed over one hipGraph of `reps` sweeps across all
- * layers' weights (as in a decode step); *bytes_out = weight bytes per launch.  Clobbers
- * decode row 0: only on an idle context. */
-int mx_llm_bench_gemv(mx_llm* ctx, int which, int reps, float* us_out, double* bytes_out);
+/* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,
+ * 1 o-proj, 2 gate/up, 3 down) for `n_rows` rows (1..max_batch), timed over one hipGraph of
+ * `reps` sweeps across all layers' weights (as in a decode step); *bytes_out = weight
+ * bytes per launch.  Clobbers decode-row state and KV position 0 of the first n_rows
+ * slots: only on an idle context. */
+int mx_llm_bench_gemv(mx_llm* ctx, int which, int n_rows, int reps, float* us_out,
+                      double* bytes_out);
 /* Diagnostic: mean microseconds of one eager attention launch (layer 0) for n_rows rows of
  * length L, `cpw` 32-position chunks per wave (split = 128*cpw), experiment flags `debug`
  * (0 = product kernel).  Clobbers decode-row state: only on an idle context. */

@@ -117,7 +117,7 @@ struct mx_llm {
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
   int att_cpw_batch = 2;        // option: same for multi-row (batched decode / prefill)
   int gemv_wpb = 4;
-  int rows_ks = 0, rows_npart = 0;  // options: multi-row GEMM K chunk / activation parts             // option: waves per block of the single-row GEMV
+  int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM K chunk / activation parts             // option: waves per block of the single-row GEMV
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
 
   template <class T>
@@ -204,18 +204,21 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->part_acc, part_rows * c.heads * 128);
   A(x->att_cnt, (size_t)x->max_rows * c.kv_heads);
   {  // multi-row GEMM workspace: the largest of the step's projections and the lm_head
+    // the tile geometry changes with the row count (16 / 32 / 64-row batch tiles), so take
+    // the largest need over every row-count class up to the maximum
     const int Rm = x->max_rows;
     const int shapes[5][4] = {{qkv_rows, c.hidden, Rm, EPI_QKV},
                               {c.hidden, c.heads * 128, Rm, EPI_RESID},
                               {2 * c.ffn, c.hidden, Rm, EPI_SILU},
                               {c.hidden, c.ffn, Rm, EPI_RESID},
                               {c.vocab, c.hidden, c.max_batch, EPI_ARGMAX}};
-    for (auto& sh : shapes) {
-      size_t wf = 0, tk = 0;
-      gemm_rows_workspace(sh[0], sh[1], sh[2], sh[3], &wf, &tk);
-      x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
-      x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
-    }
+    for (auto& sh : shapes)
+      for (int r : {16, 32, 64, sh[2]}) {
+        size_t wf = 0, tk = 0;
+        gemm_rows_workspace(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
+        x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
+        x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
+      }
   }
   A(x->rows_ws, std::max<size_t>(x->rows_ws_floats, 1));
   A(x->rows_tickets, x->rows_tickets_n);
@@ -437,7 +440,7 @@ struct RowSet {
 };
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
-  g.rows_ks = x->rows_ks;
+  g.rows_dbg = x->rows_dbg;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -739,18 +742,26 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
 // residual / KV scratch written are meaningless).  Sweeping every layer keeps the stream
 // out of the 256 MB Infinity Cache, as in a real step.  Writes mean microseconds per
 // launch (inter-kernel gap in the graph included) and the weight bytes of one launch.
-extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int reps, float* us_out,
+extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, float* us_out,
                                  double* bytes_out) {
   if (!x || !us_out || which < 0 || which > 3 || reps < 1) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
+  if (n_rows < 1 || n_rows > c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
   const int H = c.hidden, QD = c.heads * 128;
   MX_TRY(x, hipSetDevice(x->device));
   hipStream_t st = x->cap;
+  if (which == 0) {  // the QKV epilogue writes K/V at (row_slot, row_pos): keep it in range
+    std::vector<int32_t> slots(n_rows), pos(n_rows, 0);
+    for (int i = 0; i < n_rows; ++i) slots[i] = i % c.max_slots;
+    MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
+    MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
+  }
   auto args = [&](int li) {
     const LayerW& l = x->L[li];
     GemvArgs g{};
-    g.R = 1; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
+    attach_ws(x, g);
+    g.R = n_rows; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
     if (which == 0) {
       g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
       g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = x->row_slot;
@@ -807,9 +818,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
-  } else if (k == "rows_ks") {
-    if (value != 0 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_ks must be 0 or 2");
-    x->rows_ks = value;
+  } else if (k == "rows_dbg") {
+    if (value != 0 && (value < 7 || value > 9)) MX_FAIL(x, MX_ERR_ARG, "rows_dbg must be 0, 7, 8 or 9");
+    x->rows_dbg = value;
   } else if (k == "rows_npart") {
     if (value != 0 && value != 2 && value != 3) MX_FAIL(x, MX_ERR_ARG, "rows_npart must be 2 or 3");
     x->rows_npart = value;

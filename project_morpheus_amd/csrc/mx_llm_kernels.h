@@ -33,7 +33,7 @@ struct GemvArgs {
   size_t ws_floats;
   int* tickets;            // R >= 2 kernel: per-tile arrival counters (zero between launches)
   size_t tickets_n;
-  int rows_ks;             // R >= 2 kernel: 2 = 512-wide K chunks (0 = default)
+  int rows_dbg;             // R >= 2 kernel timing experiments (0 = product; results invalid otherwise)
   int rows_npart;          // R >= 2 kernel: activation bf16 parts (2 or 3; 0 = 3)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]

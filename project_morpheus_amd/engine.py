@@ -102,11 +102,11 @@ class LlmEngine:
 
     GEMV_KINDS = {"qkv": 0, "o_proj": 1, "gate_up": 2, "down": 3}
 
-    def bench_gemv(self, which: str, reps: int = 4):
-        """(mean µs per launch, weight bytes per launch) of a single-row GEMV, timed in a
-        hipGraph sweeping all layers (roofline probe; idle context only)."""
+    def bench_gemv(self, which: str, reps: int = 4, n_rows: int = 1):
+        """(mean µs per launch, weight bytes per launch) of the ``n_rows``-row decode
+        GEMV/GEMM, timed in a hipGraph sweeping all layers (roofline probe; idle context)."""
         us, nb = C.c_float(0.0), C.c_double(0.0)
-        self._check(self.lib.mx_llm_bench_gemv(self.h, self.GEMV_KINDS[which], reps,
+        self._check(self.lib.mx_llm_bench_gemv(self.h, self.GEMV_KINDS[which], n_rows, reps,
                                                C.byref(us), C.byref(nb)))
         return us.value, nb.value
 

@@ -15,16 +15,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 2, "gemv_wpb": 4, "rpw_o": 0,
-            "rpw_gu": 0, "rpw_down": 0, "rows_ks": 0, "rows_npart": 0}
+            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0}
 VARIANTS = {
     "base": {},
     "att_cpw2": {"att_cpw": 2},
     "att_cpw4": {"att_cpw": 4},
     "rpw_gu4": {"rpw_gu": 4},
     "att_cpw_batch1": {"att_cpw_batch": 1},
-    "rows_ks2": {"rows_ks": 2},
+    "rows_dbg9": {"rows_dbg": 9},
+    "rows_dbg8": {"rows_dbg": 8},
     "rows_np2": {"rows_npart": 2},
-    "rows_ks2_np2": {"rows_ks": 2, "rows_npart": 2},
     "att_cpw_batch4": {"att_cpw_batch": 4},
 }
 

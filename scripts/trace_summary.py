@@ -14,11 +14,16 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--kernel", default="")
     ap.add_argument("--bins", type=int, default=10)
+    ap.add_argument("--by-grid", action="store_true", help="split each kernel by grid size")
     args = ap.parse_args()
     by = {}
     with open(args.trace) as fh:
         for r in csv.DictReader(fh):
             name = r.get("Kernel_Name") or r.get("Name")
+            if args.by_grid:
+                grid = [r.get(k) for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z", "Grid_Size")
+                        if r.get(k)]
+                name = f"{name[:70]} grid={'x'.join(grid)}"
             if args.kernel and args.kernel not in name:
                 continue
             t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -31,7 +36,7 @@ def main():
             continue
         step = n // args.bins
         bins = [round(statistics.mean(d[i * step:(i + 1) * step]), 2) for i in range(args.bins)]
-        print(f"{name[:60]:60s} n={n:7d} mean={statistics.mean(d):8.2f}us bins={bins}")
+        print(f"{name[:110]:110s} n={n:7d} mean={statistics.mean(d):8.2f}us bins={bins}")
 
 
 if __name__ == "__main__":
