@@ -203,14 +203,15 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a, int kr, int 
 
   const size_t rowq = F8 ? (size_t)a.K / 16 : (size_t)a.K / 8;  // row length in 16-byte units
   const size_t kq0 = F8 ? (size_t)k0 / 16 : (size_t)k0 / 8;
-  const int dbg = a.rows_dbg;  // timing experiments only: 7 = timestamps, 9 = tile-contiguous
-                               // weight addressing (results invalid), 8 = skip the staging
-  const int wstep = dbg == 9 ? 64 : 4;  // uint4 units between consecutive weight loads
+  // timing experiments only (results invalid unless 0; bit flags): 1 timestamps, 2 skip the
+  // activation staging, 4 tile-contiguous weight addressing
+  const int dbg = a.rows_dbg;
+  const int wstep = (dbg & 4) ? 64 : 4;  // uint4 units between consecutive weight loads
   uint4 wv[LS][MT];
   const uint4* wp[MT];
   // loads [LO, HI) of tile t (branch-free: a short range re-reads its last step)
   auto wbase = [&](int t, int mt) -> const uint4* {
-    if (dbg == 9) {
+    if (dbg & 4) {
       const size_t rg = (size_t)min(t * MT + mt, (a.N - 1) / 16);
       return static_cast<const uint4*>(a.W) + (rg * (rowq / 4) + kq0 / 4) * 64 + lane;
     }
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a, int kr, int 
     for (int nt = 0; nt < NT; ++nt) ssp[nt] = 0.f;
     const int jg = lane & 3, cc = lane >> 2;
     const int items = NT * ks;
-    for (int u0 = dbg == 8 ? items : w; u0 < items; u0 += 8 * U) {
+    for (int u0 = (dbg & 2) ? items : w; u0 < items; u0 += 8 * U) {
       float4 xr[U][2], nr[U][2];
 #pragma unroll
       for (int i = 0; i < U; ++i) {
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a, int kr, int 
       t = tn;
     }
   }
-  if (dbg == 7 && lane == 0 && (blockIdx.x == 0 || blockIdx.x == nb - 1 || blockIdx.x == nb / 2) &&
+  if ((dbg & 1) && lane == 0 && (blockIdx.x == 0 || blockIdx.x == nb - 1 || blockIdx.x == nb / 2) &&
       (w == 0 || w == 7)) {
     const unsigned long long te = __builtin_amdgcn_s_memrealtime();
     printf("TS b%d y%d w%d tiles %d: t0 %llu staged +%llu tile1 +%llu end +%llu\n", blockIdx.x,

@@ -15,15 +15,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 2, "gemv_wpb": 4, "rpw_o": 0,
-            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0}
+            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0,
+            "prefetch_kb": 0, "prefetch_blocks": 128}
 VARIANTS = {
     "base": {},
+    "pf8m": {"prefetch_kb": 8192},
+    "pf19m": {"prefetch_kb": 19456},
+    "pf40m": {"prefetch_kb": 40960},
+    "pf64m": {"prefetch_kb": 65536},
+    "pf19m_b64": {"prefetch_kb": 19456, "prefetch_blocks": 64},
+    "pf19m_b256": {"prefetch_kb": 19456, "prefetch_blocks": 256},
     "att_cpw2": {"att_cpw": 2},
     "att_cpw4": {"att_cpw": 4},
     "rpw_gu4": {"rpw_gu": 4},
     "att_cpw_batch1": {"att_cpw_batch": 1},
-    "rows_dbg9": {"rows_dbg": 9},
-    "rows_dbg8": {"rows_dbg": 8},
+    "rows_contig": {"rows_dbg": 4},
+    "rows_nostage": {"rows_dbg": 2},
     "rows_np2": {"rows_npart": 2},
     "att_cpw_batch4": {"att_cpw_batch": 4},
 }

@@ -27,7 +27,7 @@ def main():
     from project_morpheus_amd.engine import LlmEngine
     from project_morpheus_amd.weights import synthetic_llm_weights
     rows = [int(r) for r in args.rows.split(",")]
-    R = max(rows + [args.profile_rows])
+    R = max(rows + [max(1, args.profile_rows)])
     cfg = C.OrpheusConfig()
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
     if args.fp8:
@@ -52,6 +52,8 @@ def main():
         print(f"rows {r}: " + json.dumps(line), flush=True)
     st = torch.cuda.Stream()
     P = args.profile_rows
+    if P <= 0:
+        return
     prompt = list(range(1000, 1020))
     for i in range(P):
         llm.prefill(i, i, prompt, 1.1, st)

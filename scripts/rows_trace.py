@@ -20,7 +20,7 @@ def main():
                     max_prefill=256)
     llm.bench_gemv(kind, reps=1, n_rows=rows)
     torch.cuda.synchronize()
-    llm.set_option("rows_dbg", 7)
+    llm.set_option("rows_dbg", 1)
     sys.stdout.flush()
     llm.bench_gemv(kind, reps=1, n_rows=rows)
     torch.cuda.synchronize()
