@@ -118,11 +118,6 @@ struct mx_llm {
   int att_cpw_batch = 2;        // option: same for multi-row (batched decode / prefill)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
-  // option "prefetch_kb": single-row decode warms the Infinity Cache with the next
-  // projections' weights on a side stream while attention (latency-bound) runs
-  int prefetch_kb = 0, prefetch_blocks = 128;
-  hipStream_t side = nullptr;
-  std::vector<hipEvent_t> fork_ev, join_ev;
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
 
   template <class T>
@@ -268,14 +263,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess)
     e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking);
-  for (int i = 0; i < c.layers && e == hipSuccess; ++i) {
-    hipEvent_t a = nullptr, b = nullptr;
-    e = hipEventCreateWithFlags(&a, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
-    x->fork_ev.push_back(a);
-    x->join_ev.push_back(b);
-  }
   if (e == hipSuccess) e = gemv_prepare(std::max(std::max(c.hidden, c.ffn), c.heads * 128));
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -482,7 +469,6 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
   const int H = c.hidden, QD = c.heads * 128;
   const int qkv_rows = QD + 2 * c.kv_heads * 128;
   hipError_t e = hipSuccess;
-  const bool pf = x->prefetch_kb > 0 && rs.R == 1 && !prof;
   for (int li = 0; li < c.layers && e == hipSuccess; ++li) {
     const LayerW& l = x->L[li];
     uint16_t* kc = x->kcache + x->kv_layer_elems * li;
@@ -496,24 +482,10 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
     g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
-    if (li > 0 && pf) e = hipStreamWaitEvent(st, x->join_ev[li - 1], 0);
-    if (e != hipSuccess) break;
     PROF_BEGIN(PK_QKV);
     e = launch_gemv(g, EPI_QKV, true, st);
     PROF_END();
     if (e != hipSuccess) break;
-    if (pf) {  // side stream: warm wo + the head of wgu while attention runs
-      const size_t ob = (size_t)x->esz * H * QD, gb = (size_t)x->esz * 2 * c.ffn * H;
-      const size_t want = (size_t)x->prefetch_kb * 1024;
-      e = hipEventRecord(x->fork_ev[li], st);
-      if (e == hipSuccess) e = hipStreamWaitEvent(x->side, x->fork_ev[li], 0);
-      if (e == hipSuccess)
-        e = launch_prefetch(l.wo, std::min(want, ob), x->prefetch_blocks, x->side);
-      if (e == hipSuccess && want > ob)
-        e = launch_prefetch(l.wgu, std::min(want - ob, gb), x->prefetch_blocks, x->side);
-      if (e == hipSuccess) e = hipEventRecord(x->join_ev[li], x->side);
-      if (e != hipSuccess) break;
-    }
     AttnArgs at{};
     at.Q = x->q; at.kcache = kc; at.vcache = vc; at.row_slot = rs.slot; at.row_pos = rs.pos;
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
@@ -553,7 +525,6 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     e = launch_gemv(d, EPI_RESID, false, st);
     PROF_END();
   }
-  if (e == hipSuccess && pf) e = hipStreamWaitEvent(st, x->join_ev[c.layers - 1], 0);
   return e;
 }
 
@@ -862,12 +833,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rpw_gu") {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
-  } else if (k == "prefetch_kb") {
-    if (value < 0 || value > 262144) MX_FAIL(x, MX_ERR_ARG, "prefetch_kb out of range");
-    x->prefetch_kb = value;
-  } else if (k == "prefetch_blocks") {
-    if (value < 1 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "prefetch_blocks out of range");
-    x->prefetch_blocks = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
     if (value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
@@ -922,9 +887,6 @@ extern "C" void mx_llm_destroy(mx_llm* x) {
   for (auto& kv : x->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : x->graph_defs) (void)hipGraphDestroy(kv.second);
   if (x->cap) (void)hipStreamDestroy(x->cap);
-  if (x->side) (void)hipStreamDestroy(x->side);
-  for (auto ev : x->fork_ev) (void)hipEventDestroy(ev);
-  for (auto ev : x->join_ev) (void)hipEventDestroy(ev);
   for (void* p : x->allocs) (void)hipFree(p);
   if (x->hist_host) (void)hipHostFree(x->hist_host);
   delete x;

@@ -922,27 +922,4 @@ hipError_t launch_to_f32(float* dst, const void* src, int64_t n, int src_bf16, h
 }
 
 
-// Cache warmer for the side stream: every thread streams 16-byte loads (default, allocating
-// policy) and folds them into a value that is stored only if it equals an impossible key, so
-// the loads cannot be elided and nothing observable is written.
-__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* p, size_t n, uint32_t* sink) {
-  uint32_t acc = 0;
-  const size_t stride = (size_t)gridDim.x * 256;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += 4 * stride) {
-    uint4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = i + j * stride < n ? p[i + j * stride] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-  }
-  if (acc == 0x9e3779b9u && sink) *sink = acc;
-}
-
-hipError_t launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st) {
-  if (!p || bytes < 16) return hipSuccess;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, st,
-                     static_cast<const uint4*>(p), bytes / 16, nullptr);
-  return hipGetLastError();
-}
-
 }  // namespace mx

@@ -90,8 +90,6 @@ void gemm_rows_workspace(int N, int K, int R, int epi, size_t* ws_floats, size_t
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);
-// Read `bytes` at p with allocating loads (warms L2 / Infinity Cache); no visible effect.
-hipError_t launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st);
 hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t* embed,

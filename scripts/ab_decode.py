@@ -15,16 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 2, "gemv_wpb": 4, "rpw_o": 0,
-            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0,
-            "prefetch_kb": 0, "prefetch_blocks": 128}
+            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0}
 VARIANTS = {
     "base": {},
-    "pf8m": {"prefetch_kb": 8192},
-    "pf19m": {"prefetch_kb": 19456},
-    "pf40m": {"prefetch_kb": 40960},
-    "pf64m": {"prefetch_kb": 65536},
-    "pf19m_b64": {"prefetch_kb": 19456, "prefetch_blocks": 64},
-    "pf19m_b256": {"prefetch_kb": 19456, "prefetch_blocks": 256},
     "att_cpw2": {"att_cpw": 2},
     "att_cpw4": {"att_cpw": 4},
     "rpw_gu4": {"rpw_gu": 4},
