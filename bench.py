@@ -41,6 +41,7 @@ def parse():
                    help="configs[2]: concurrent streams per GPU (0 skips it)")
     p.add_argument("--fp8-batch", type=int, default=8,
                    help="configs[4]: fp8 streams per GPU (0 skips the fp8 section)")
+    p.add_argument("--no-http", action="store_true", help="skip the HTTP-level line")
     p.add_argument("--long-read-docs", type=int, default=16,
                    help="configs[3]: long_read documents (0 skips it)")
     p.add_argument("--step-pos", type=int, default=600,
@@ -151,6 +152,69 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
             "audio_seconds": round(audio, 2),
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
             "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
+
+
+def run_http(args, syn, prompt_text, inject, local):
+    """configs[1] at the HTTP level: one ``POST /v1/audio/speech`` through the ASGI app of
+    ``project_morpheus_amd.server`` (no sockets; the app's own adapter and streaming body),
+    the adapter's source bound to this process's engine.  RTF = audio / wall from request
+    start to the last body chunk; first audio = first non-empty PCM chunk after the header."""
+    import asyncio
+    import json as _json
+
+    import torch
+
+    from project_morpheus_amd import inference as I
+    from project_morpheus_amd.adapter import MxTTSAdapter
+    from project_morpheus_amd.server import build_app
+    from project_morpheus_amd.tokenizer import Tokenizer
+    tok = Tokenizer(None)
+
+    class BenchAdapter(MxTTSAdapter):
+        @staticmethod
+        def source(prompt, voice, use_batching, max_batch_chars, cancel):
+            torch.cuda.set_device(local)
+            ids = I.prompt_ids(tok.encode(f"{voice}: {prompt}"))
+            for pcm in syn.run(ids, args.max_tokens, 1.1, stop_ids=(), inject_ids=inject):
+                if cancel.is_set():
+                    return
+                yield pcm
+
+    app = build_app(adapter_cls=BenchAdapter)
+
+    async def one():
+        body = _json.dumps({"input": prompt_text, "voice": "tara"}).encode()
+        sent = {"done": False}
+        marks = []
+
+        async def receive():
+            if not sent["done"]:
+                sent["done"] = True
+                return {"type": "http.request", "body": body, "more_body": False}
+            await asyncio.sleep(3600)
+            return {"type": "http.disconnect"}
+
+        async def send(msg):
+            if msg["type"] == "http.response.body":
+                marks.append((time.perf_counter(), len(msg.get("body", b""))))
+
+        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1",
+                 "method": "POST", "scheme": "http", "path": "/v1/audio/speech",
+                 "raw_path": b"/v1/audio/speech", "query_string": b"", "root_path": "",
+                 "headers": [(b"content-type", b"application/json")],
+                 "client": ("127.0.0.1", 1), "server": ("127.0.0.1", 80)}
+        t0 = time.perf_counter()
+        await app(scope, receive, send)
+        return t0, marks
+
+    asyncio.run(one())  # warm
+    t0, marks = asyncio.run(one())
+    pcm = sum(n for _, n in marks) - 44
+    first = next(t for t, n in marks[1:] if n > 0) if len(marks) > 1 else t0
+    wall = marks[-1][0] - t0
+    return {"workload": "configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream)",
+            "value": round(pcm / 2 / 24000.0 / wall, 3), "unit": "audio-sec/wall-sec",
+            "first_audio_ms": round(1e3 * (first - t0), 2), "bytes": pcm}
 
 
 def run_long_read(args, llm, snac, rank, world, dist):
@@ -310,6 +374,11 @@ def main():
         dist.all_gather_object(fl, firsts)
         firsts = [x for r in fl for x in r]
 
+    # ---- configs[1] at the HTTP level (rank 0 only: one request through the ASGI app) ----
+    http_level = None
+    if rank == 0 and not args.no_http:
+        http_level = run_http(args, syn, "Hello world", inject, local)
+
     # ---- configs[2]: B concurrent streams per GPU, continuous batching + batched SNAC ----
     batched = None
     if B3 > 0:
@@ -379,6 +448,7 @@ def main():
                        "max_tokens": args.max_tokens, "parallelism": f"streams{world}"},
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
             "audio_seconds": round(audio, 3),
+            "http_level": http_level,
             "configs_2_batched": batched,
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,

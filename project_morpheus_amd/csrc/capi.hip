@@ -115,9 +115,11 @@ struct mx_llm {
   float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
-  int att_cpw_batch = 2;        // option: same for multi-row (batched decode / prefill)
+  int att_cpw_batch = 1;        // option: same for multi-row (batched decode / prefill)
+  int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
+  int rows_kernel = 4;               // option: multi-row GEMM generation (4 = measured faster, 5)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
 
   template <class T>
@@ -216,6 +218,9 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
       for (int r : {16, 32, 64, sh[2]}) {
         size_t wf = 0, tk = 0;
         gemm_rows_workspace(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
+        x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
+        x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
+        v4::gemm_rows_workspace_v4(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
         x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
         x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
       }
@@ -441,6 +446,7 @@ struct RowSet {
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_dbg = x->rows_dbg;
+  g.rows_kernel = x->rows_kernel;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -491,6 +497,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
     at.scale = 1.0f / sqrtf(128.0f);
     at.cpw = rs.R == 1 ? x->att_cpw_b1 : x->att_cpw_batch;
+    at.nw = rs.R == 1 ? x->att_nw_b1 : x->att_nw_batch;
     at.split_stride = c.max_pos / ATT_S_MIN;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
     at.out = x->att;
@@ -635,7 +642,8 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
-  const int S = ATT_S_MIN * (n_rows == 1 ? x->att_cpw_b1 : x->att_cpw_batch);
+  const int S = 32 * (n_rows == 1 ? x->att_nw_b1 * x->att_cpw_b1
+                                  : x->att_nw_batch * x->att_cpw_batch);
   const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
   const int key = n_rows * 4096 + nsplit;
   auto it = x->graphs.find(key);
@@ -702,6 +710,7 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
   at.Q = x->q; at.kcache = x->kcache; at.vcache = x->vcache; at.row_slot = x->row_slot;
   at.row_pos = x->row_pos; at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
   at.scale = 1.0f / sqrtf(128.0f); at.cpw = cpw; at.split_stride = c.max_pos / ATT_S_MIN;
+  at.nw = n_rows == 1 ? x->att_nw_b1 : x->att_nw_batch;
   at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt; at.out = x->att;
   at.debug = debug;
   MX_TRY(x, launch_attention(at, n_rows, L, st));  // warm + argument check
@@ -833,6 +842,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rpw_gu") {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
+  } else if (k == "rows_kernel") {
+    if (value != 4 && value != 5) MX_FAIL(x, MX_ERR_ARG, "rows_kernel must be 4 or 5");
+    x->rows_kernel = value;
+  } else if (k == "att_nw" || k == "att_nw_batch") {
+    if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
+    (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
     if (value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;

@@ -452,9 +452,15 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
   f2 = __builtin_bit_cast(bf16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
 }
 
-template <int GRP, int CPW>
-__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
-  constexpr int S = 128 * CPW;
+// One block = NW waves over S = 32 NW CPW positions of one (row, kv head); wave w takes the
+// CPW consecutive 32-position chunks starting at 32 (w CPW), with the next chunk's K / V^T
+// loads in flight under the current chunk's MFMAs and softmax.  NW = 8, CPW = 4 covers
+// 1,024 positions in one block, so a single-row step up to that length needs no split merge.
+template <int GRP, int CPW, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
+  constexpr int S = 32 * NW * CPW;
+  constexpr int NT = NW * 64;
+  constexpr int KM = (GRP * 128 + NT - 1) / NT;  // (head, dim) outputs per thread in merges
   const int split = blockIdx.x, kvh = blockIdx.y, r = blockIdx.z;
   const int L = a.row_pos[r] + 1;
   const int nsplit = (L + S - 1) / S;
@@ -465,6 +471,24 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const size_t head = (size_t)slot * a.kv_heads + kvh;
   const uint4* K = reinterpret_cast<const uint4*>(a.kcache) + head * a.max_pos * 16;
   const uint16_t* VT = a.vcache + head * 128 * a.max_pos;
+  const int rr = lane & 15;
+
+  // K fragments (A operand): tile T, MFMA row rr -> position 8(rr>>2) + 4T + (rr&3);
+  // V^T fragments (B operand): lane (dim 16 t + c, group g) <- positions base + 8g .. +8
+  uint4 kf[2][2][4], vf[2][8];
+  auto load_kv = [&](int base, int b) {
+#pragma unroll
+    for (int T = 0; T < 2; ++T) {
+      const int p = min(base + 8 * (rr >> 2) + 4 * T + (rr & 3), L - 1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) kf[b][T][st] = K[(size_t)p * 16 + 4 * st + g];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      vf[b][t] = *reinterpret_cast<const uint4*>(VT + (size_t)(16 * t + c) * a.max_pos + base + 8 * g);
+  };
+  const int base0 = split * S + wid * CPW * 32;
+  if (base0 < L) load_kv(base0, 0);
 
   // Q^T fragments: lane (col c = head, group g) holds q[c][32 s + 8 g + j], 3 bf16 parts
   bf16x8 qf[3][4];
@@ -490,23 +514,12 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   f32x4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int rr = lane & 15;
+#pragma unroll
   for (int ch = 0; ch < CPW; ++ch) {
-    const int base = split * S + (wid * CPW + ch) * 32;
+    const int cb = ch & 1;
+    const int base = base0 + ch * 32;
     if (base >= L) break;  // wave-uniform
-    // K fragments (A operand): tile T, MFMA row rr -> position 8(rr>>2) + 4T + (rr&3)
-    uint4 kf[2][4];
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      const int p = min(base + 8 * (rr >> 2) + 4 * T + (rr & 3), L - 1);
-#pragma unroll
-      for (int st = 0; st < 4; ++st) kf[T][st] = K[(size_t)p * 16 + 4 * st + g];
-    }
-    // V^T fragments (B operand): lane (dim 16 t + c, group g) <- positions base + 8g .. +8
-    uint4 vf[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-      vf[t] = *reinterpret_cast<const uint4*>(VT + (size_t)(16 * t + c) * a.max_pos + base + 8 * g);
+    if (ch + 1 < CPW && base + 32 < L) load_kv(base + 32, cb ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     // scores
     f32x4 sc[2];
@@ -515,20 +528,20 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       sc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        const bf16x8 kb = __builtin_bit_cast(bf16x8, kf[T][st]);
+        const bf16x8 kb = __builtin_bit_cast(bf16x8, kf[cb][T][st]);
 #pragma unroll
         for (int pt = 0; pt < 3; ++pt)
           sc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb, qf[pt][st], sc[T], 0, 0, 0);
       }
     }
     // online softmax: this lane holds head c, positions base + 8g + j (j = 4T + i)
-    float s[8];
+    float sv[8];
     float mc = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int p = base + 8 * g + j;
-      s[j] = p < L ? sc[j >> 2][j & 3] * a.scale : -INFINITY;
-      mc = fmaxf(mc, s[j]);
+      sv[j] = p < L ? sc[j >> 2][j & 3] * a.scale : -INFINITY;
+      mc = fmaxf(mc, sv[j]);
     }
     mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
     mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     float pv[8], ps = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      pv[j] = expf(s[j] - Mn);
+      pv[j] = expf(sv[j] - Mn);
       ps += pv[j];
     }
     ps += __shfl_xor(ps, 16, 64);
@@ -555,15 +568,15 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     split3(pv, pf[0], pf[1], pf[2]);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const bf16x8 vb = __builtin_bit_cast(bf16x8, vf[t]);
+      const bf16x8 vb = __builtin_bit_cast(bf16x8, vf[cb][t]);
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt)
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt], vb, acc[t], 0, 0, 0);
     }
   }
 
-  __shared__ __attribute__((aligned(16))) float wacc[4][GRP][128];
-  __shared__ float wml[4][GRP][2];
+  __shared__ __attribute__((aligned(16))) float wacc[NW][GRP][128];
+  __shared__ float wml[NW][GRP][2];
   __shared__ float sml[ATT_MAX_SPLITS][GRP][2];
   __shared__ int last_s;
   // (M, lsum) of head c sit in lanes c (any g); O^T row h = 4 g + i, dim 16 t + c
@@ -578,19 +591,20 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       for (int t = 0; t < 8; ++t) wacc[wid][i][16 * t + c] = acc[t][i];
   }
   __syncthreads();
-  // block merge: thread -> (head tid / 128 (+2), dim tid % 128)
-  const int th = tid >> 7, td = tid & 127;
-  float bm[2] = {0.f, 0.f}, bl[2] = {0.f, 0.f}, bn[2] = {0.f, 0.f};
+  // block merge: thread -> outputs (head, dim) = idx / 128, idx % 128 for idx = tid + NT k
+  float bm[KM], bl[KM], bn[KM];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int h = th + 2 * k;
-    if (h < GRP) {
+  for (int k = 0; k < KM; ++k) {
+    bm[k] = bl[k] = bn[k] = 0.f;
+    const int idx = tid + NT * k;
+    if (idx < GRP * 128) {
+      const int h = idx >> 7, td = idx & 127;
       float Mb = -INFINITY;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) Mb = fmaxf(Mb, wml[w][h][0]);
+      for (int w = 0; w < NW; ++w) Mb = fmaxf(Mb, wml[w][h][0]);
       float num = 0.f, den = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         const float mw = wml[w][h][0];
         const float f = (mw == -INFINITY) ? 0.f : expf(mw - Mb);
         num = fmaf(f, wacc[w][h][td], num);
@@ -604,18 +618,19 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   float* out = a.out + ((size_t)r * a.heads + kvh * GRP) * 128;
   if (nsplit == 1) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int h = th + 2 * k;
-      if (h < GRP) out[h * 128 + td] = bn[k] / bl[k];
+    for (int k = 0; k < KM; ++k) {
+      const int idx = tid + NT * k;
+      if (idx < GRP * 128) out[idx] = bn[k] / bl[k];
     }
     return;
   }
   // publish this split's partial (write-through), then take a ticket
   const size_t pb = ((size_t)r * a.kv_heads + kvh) * a.split_stride;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int h = th + 2 * k;
-    if (h < GRP) {
+  for (int k = 0; k < KM; ++k) {
+    const int idx = tid + NT * k;
+    if (idx < GRP * 128) {
+      const int h = idx >> 7, td = idx & 127;
       st_wt(a.part_acc + ((pb + split) * GRP + h) * 128 + td, bn[k]);
       if (td == 0) {
         st_wt(a.part_ml + ((pb + split) * GRP + h) * 2, bm[k]);
@@ -634,24 +649,25 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   }
   __syncthreads();
   if (!last_s) return;
-  // last arriver: the (m, l) pairs and this thread's accumulator column of every split are
+  // last arriver: the (m, l) pairs and this thread's accumulator columns of every split are
   // loaded in ONE round trip (ATT_MERGE_CHUNK splits at a time), then merged.
-  for (int i = tid; i < nsplit * GRP * 2; i += 256)
+  for (int i = tid; i < nsplit * GRP * 2; i += NT)
     (&sml[0][0][0])[i] = ld_wt(a.part_ml + pb * GRP * 2 + i);
-  float col[2][ATT_MERGE_CHUNK];
+  float col[KM][ATT_MERGE_CHUNK];
   const int n0 = min(nsplit, ATT_MERGE_CHUNK);
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int h = min(th + 2 * k, GRP - 1);
+  for (int k = 0; k < KM; ++k) {
+    const int idx = min(tid + NT * k, GRP * 128 - 1);
 #pragma unroll
     for (int sp = 0; sp < ATT_MERGE_CHUNK; ++sp)
-      col[k][sp] = ld_wt(a.part_acc + ((pb + min(sp, n0 - 1)) * GRP + h) * 128 + td);
+      col[k][sp] = ld_wt(a.part_acc + ((pb + min(sp, n0 - 1)) * GRP) * 128 + idx);
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int h = th + 2 * k;
-    if (h >= GRP) continue;
+  for (int k = 0; k < KM; ++k) {
+    const int idx = tid + NT * k;
+    if (idx >= GRP * 128) continue;
+    const int h = idx >> 7;
     float Mb = -INFINITY;
     for (int sp = 0; sp < nsplit; ++sp) Mb = fmaxf(Mb, sml[sp][h][0]);
     float num = 0.f, den = 0.f;
@@ -665,10 +681,10 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     }
     for (int sp = ATT_MERGE_CHUNK; sp < nsplit; ++sp) {  // long contexts only
       const float f = expf(sml[sp][h][0] - Mb);
-      num = fmaf(f, ld_wt(a.part_acc + ((pb + sp) * GRP + h) * 128 + td), num);
+      num = fmaf(f, ld_wt(a.part_acc + ((pb + sp) * GRP) * 128 + idx), num);
       den = fmaf(f, sml[sp][h][1], den);
     }
-    out[h * 128 + td] = num / den;
+    out[idx] = num / den;
   }
 }
 
@@ -832,7 +848,8 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
-    const hipError_t e = launch_gemm_rows(a, epi, norm, st);
+    const hipError_t e = a.rows_kernel == 4 ? v4::launch_gemm_rows_v4(a, epi, norm, st)
+                                            : launch_gemm_rows(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
   }
   // RT = 1 for the decode batch of 1; RT = 4 otherwise (prefill / batched decode).
@@ -881,18 +898,21 @@ hipError_t gemv_prepare(int kmax) {
 }
 
 hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st) {
-  const int S = 128 * a.cpw;
+  const int nw = a.nw == 8 ? 8 : 4;
+  const int S = 32 * nw * a.cpw;
   const int nsplit = (max_len + S - 1) / S;
   if (nsplit > ATT_MAX_SPLITS || (a.max_pos + S - 1) / S > a.split_stride || a.max_pos % 8)
     return hipErrorInvalidValue;
   const dim3 grid(nsplit, a.kv_heads, R);
-#define MX_AT(G_, C_)                                                              \
-  if (a.heads / a.kv_heads == G_ && a.cpw == C_) {                                 \
-    hipLaunchKernelGGL((attn_kernel<G_, C_>), grid, dim3(256), 0, st, a);          \
-    return hipGetLastError();                                                      \
+#define MX_AT(G_, C_, W_)                                                            \
+  if (a.heads / a.kv_heads == G_ && a.cpw == C_ && nw == W_) {                       \
+    hipLaunchKernelGGL((attn_kernel<G_, C_, W_>), grid, dim3(64 * W_), 0, st, a);    \
+    return hipGetLastError();                                                        \
   }
-  MX_AT(1, 1) MX_AT(1, 2) MX_AT(1, 4) MX_AT(2, 1) MX_AT(2, 2) MX_AT(2, 4)
-  MX_AT(3, 1) MX_AT(3, 2) MX_AT(3, 4) MX_AT(4, 1) MX_AT(4, 2) MX_AT(4, 4)
+#define MX_ATG(G_) MX_AT(G_, 1, 4) MX_AT(G_, 2, 4) MX_AT(G_, 4, 4) \
+                   MX_AT(G_, 1, 8) MX_AT(G_, 2, 8) MX_AT(G_, 4, 8)
+  MX_ATG(1) MX_ATG(2) MX_ATG(3) MX_ATG(4)
+#undef MX_ATG
 #undef MX_AT
   return hipErrorInvalidValue;
 }

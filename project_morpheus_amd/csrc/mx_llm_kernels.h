@@ -8,7 +8,7 @@ namespace mx {
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SILU = 2, EPI_QKV = 3, EPI_ARGMAX = 4 };
 enum { WT_BF16 = 0, WT_FP8 = 1 };  // weight storage: bf16, or OCP e4m3 + fp32 scale per row
 
-constexpr int ATT_S_MIN = 128;      // smallest split (positions) = 4 waves x 32
+constexpr int ATT_S_MIN = 128;      // smallest split (positions) = 4 waves x 32 x 1 chunk
 constexpr int ATT_MAX_SPLITS = 256; // splits one launch may merge
 constexpr int ATT_MAXG = 4;         // max q-heads per kv-head
 constexpr int ATT_MERGE_CHUNK = 16; // splits whose partials the merging block prefetches
@@ -35,6 +35,7 @@ struct GemvArgs {
   size_t tickets_n;
   int rows_dbg;             // R >= 2 kernel timing experiments (0 = product; results invalid otherwise)
   int rows_npart;          // R >= 2 kernel: activation bf16 parts (2 or 3; 0 = 3)
+  int rows_kernel;         // R >= 2 kernel generation: 4 = llm_batched_v4.hip (default), 5
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -58,7 +59,8 @@ struct AttnArgs {
   const int32_t* row_slot;
   const int32_t* row_pos;
   int heads, kv_heads, max_pos;
-  int cpw;                 // 32-position chunks per wave: split = 128 * cpw positions
+  int cpw;                 // 32-position chunks per wave: split = 32 * nw * cpw positions
+  int nw;                  // waves per block (4 or 8; 0 = 4)
   int split_stride;        // partial slots per (row, kv-head) >= max_pos / split
   float scale;
   float* part_ml;          // [R][kv_heads][nsplit_max][grp][2]  (m, l) per split
@@ -87,6 +89,10 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 // R >= 2 rows on bf16 MFMA (llm_batched.hip); hipErrorNotSupported if the shape is not covered
 hipError_t launch_gemm_rows(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
+namespace v4 {  // multi-row GEMM generation 4 (llm_batched_v4.hip): the default product path
+hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
+void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
+}  // namespace v4
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);

@@ -14,10 +14,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 2, "gemv_wpb": 4, "rpw_o": 0,
-            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0}
+DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 1, "att_nw": 4, "att_nw_batch": 8, "gemv_wpb": 4, "rpw_o": 0,
+            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0, "rows_kernel": 4}
 VARIANTS = {
     "base": {},
+    "rows_v5": {"rows_kernel": 5},
+    "att_b_nw4cpw2": {"att_nw_batch": 4, "att_cpw_batch": 2},
     "att_cpw2": {"att_cpw": 2},
     "att_cpw4": {"att_cpw": 4},
     "rpw_gu4": {"rpw_gu": 4},

@@ -16,12 +16,14 @@ def main():
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
     llm = LlmEngine(cfg, w, device=0, max_slots=32, max_pos=2048, max_batch=32, max_prefill=64)
     out = {}
-    for rows in (1, 32):
-        for cpw in (1, 2, 4):
-            key = f"rows{rows}_cpw{cpw}"
-            out[key] = {L: round(llm.bench_attention(L, rows, cpw, 0), 2)
-                        for L in (64, 128, 256, 512, 1024, 2048)}
-            print(key, json.dumps(out[key]), flush=True)
+    for rows in (1, 8, 32):
+        for nw in (4, 8):
+            llm.set_option("att_nw" if rows == 1 else "att_nw_batch", nw)
+            for cpw in (1, 2, 4):
+                key = f"rows{rows}_nw{nw}_cpw{cpw}"
+                out[key] = {L: round(llm.bench_attention(L, rows, cpw, 0), 2)
+                            for L in (64, 256, 512, 640, 1024, 1280, 2048)}
+                print(key, json.dumps(out[key]), flush=True)
 
 
 if __name__ == "__main__":

@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--kernel", default="")
     ap.add_argument("--bins", type=int, default=10)
     ap.add_argument("--by-grid", action="store_true", help="split each kernel by grid size")
+    ap.add_argument("--gaps", action="store_true",
+                    help="also print the mean idle gap before each kernel (same queue)")
     args = ap.parse_args()
     by = {}
     with open(args.trace) as fh:
@@ -28,6 +30,20 @@ def main():
                 continue
             t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             by.setdefault(name, []).append((int(r["Start_Timestamp"]), t))
+    if args.gaps:
+        rows = []
+        with open(args.trace) as fh:
+            for r in csv.DictReader(fh):
+                name = r.get("Kernel_Name") or r.get("Name")
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+        rows.sort()
+        gaps = {}
+        for (s0, e0, _), (s1, e1, n1) in zip(rows, rows[1:]):
+            g = (s1 - e0) / 1e3
+            if 0 <= g < 50:  # same burst (graph replay), not host idle time
+                gaps.setdefault(n1[:60], []).append(g)
+        for n, v in sorted(gaps.items(), key=lambda kv: -len(kv[1])):
+            print(f"gap before {n:60s} n={len(v):7d} mean={statistics.mean(v):6.2f}us")
     for name, v in by.items():
         v.sort()
         d = [t for _, t in v]
