@@ -105,6 +105,15 @@ int mx_llm_bench_attention(mx_llm* ctx, int L, int n_rows, int cpw, int debug, i
 int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
 /* Host-mapped token history [max_slots][max_pos] int32 written by the device. */
 int32_t* mx_llm_history(mx_llm* ctx);
+/* Persistent one-row decode step (one launch for all layers, Orpheus-3B shapes only):
+ * *eligible = 1 when one-row mx_llm_decode graphs use it (option "mega", shape and
+ * co-residency checks); *status = its last launch's give-up code (0 = every in-launch
+ * hand-off completed).  Synchronises `stream`. */
+int mx_llm_mega_info(mx_llm* ctx, int* eligible, int* status, void* stream);
+/* Diagnostics (option "mega_trace" = 1): copy the per-block, per-layer event wall clocks
+ * (100 MHz) of the last persistent step, [256 blocks][layers][16 events]; returns the count
+ * copied or a negative error.  Synchronises the device. */
+int64_t mx_llm_mega_trace(mx_llm* ctx, int64_t* host_out, int64_t n);
 /* Parity/debug: keep a copy of the penalised logits of each decode row (enable before the
  * first mx_llm_decode; costs one extra write per vocab entry) and read one row back. */
 int mx_llm_debug_logits(mx_llm* ctx, int enable);

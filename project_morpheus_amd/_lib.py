@@ -58,6 +58,8 @@ _SIGS = {
                                          C.POINTER(C.c_float)]),
     "mx_llm_release_row": (C.c_int, [_P, C.c_int, _P]),
     "mx_llm_history": (C.POINTER(C.c_int32), [_P]),
+    "mx_llm_mega_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), _P]),
+    "mx_llm_mega_trace": (C.c_int64, [_P, C.POINTER(C.c_int64), C.c_int64]),
     "mx_llm_debug_logits": (C.c_int, [_P, C.c_int]),
     "mx_llm_read_logits": (C.c_int, [_P, C.c_int, _P, _P]),
     "mx_llm_last_error": (C.c_char_p, [_P]),

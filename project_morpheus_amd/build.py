@@ -11,8 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmorpheus_mx.so")
-SOURCES = ["capi.hip", "llm_kernels.hip", "llm_batched.hip", "llm_batched_v4.hip",
-           "snac_kernels.hip"]
+SOURCES = ["capi.hip", "llm_kernels.hip", "llm_batched.hip", "llm_batched_v4.hip", "llm_mega.hip",
+           "llm_batched_v7.hip", "snac_kernels.hip"]
 HEADERS = ["mx_common.h", "mx_llm_kernels.h", "mx_snac_kernels.h"]
 ARCH = os.environ.get("MORPHEUS_MX_ARCH", "gfx950")
 

@@ -119,8 +119,23 @@ struct mx_llm {
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
-  int rows_kernel = 4;               // option: multi-row GEMM generation (4 = measured faster, 5)
+  int rows_kernel = 4;               // option: multi-row GEMM generation (4 measured fastest; 7, 5)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
+  // persistent single-stream step (llm_mega.hip): eligible shapes + co-residency checked at
+  // create; option "mega" (default 0) picks it for one-row decode graphs
+  bool mega_ok = false;
+  int mega = 0, mega_ring = 32;  // measured slower than the per-kernel step
+  float *mega_ws = nullptr, *mega_part = nullptr, *h_fin = nullptr;
+  int* mega_sync = nullptr;
+  size_t mega_sync_bytes = 0;
+  void* mega_dummy = nullptr;
+  int mega_nsplit_cap = 0;
+  long long* mega_trace = nullptr;  // option "mega_trace": per-block event clocks of the last step
+  // every layer's matrices / norms / fp8 scales of one kind are contiguous (the persistent
+  // kernel walks layers by a fixed stride)
+  void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
+  float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
+  float *attn_norm_all = nullptr, *mlp_norm_all = nullptr;
 
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -178,18 +193,34 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (!c.tied || f8) AM(x->lm, c.vocab, c.hidden);
   if (f8) A(x->slm, c.vocab);
   A(x->norm, c.hidden);
-  for (auto& l : x->L) {
-    A(l.attn_norm, c.hidden);
-    A(l.mlp_norm, c.hidden);
-    AM(l.wqkv, qkv_rows, c.hidden);
-    AM(l.wo, c.hidden, c.heads * 128);
-    AM(l.wgu, 2 * c.ffn, c.hidden);
-    AM(l.wd, c.hidden, c.ffn);
-    if (f8) {
-      A(l.sqkv, qkv_rows);
-      A(l.so, c.hidden);
-      A(l.sgu, 2 * c.ffn);
-      A(l.sd, c.hidden);
+  const size_t NL = (size_t)c.layers;
+  A(x->attn_norm_all, NL * c.hidden);
+  A(x->mlp_norm_all, NL * c.hidden);
+  AM(x->wqkv_all, NL * qkv_rows, c.hidden);
+  AM(x->wo_all, NL * c.hidden, c.heads * 128);
+  AM(x->wgu_all, NL * 2 * c.ffn, c.hidden);
+  AM(x->wd_all, NL * c.hidden, c.ffn);
+  if (f8) {
+    A(x->sqkv_all, NL * qkv_rows);
+    A(x->so_all, NL * c.hidden);
+    A(x->sgu_all, NL * 2 * c.ffn);
+    A(x->sd_all, NL * c.hidden);
+  }
+  if (e == hipSuccess) {
+    for (size_t li = 0; li < NL; ++li) {
+      LayerW& l = x->L[li];
+      l.attn_norm = x->attn_norm_all + li * c.hidden;
+      l.mlp_norm = x->mlp_norm_all + li * c.hidden;
+      l.wqkv = (uint8_t*)x->wqkv_all + li * qkv_rows * c.hidden * x->esz;
+      l.wo = (uint8_t*)x->wo_all + li * c.hidden * c.heads * 128 * x->esz;
+      l.wgu = (uint8_t*)x->wgu_all + li * 2 * c.ffn * c.hidden * x->esz;
+      l.wd = (uint8_t*)x->wd_all + li * c.hidden * c.ffn * x->esz;
+      if (f8) {
+        l.sqkv = x->sqkv_all + li * qkv_rows;
+        l.so = x->so_all + li * c.hidden;
+        l.sgu = x->sgu_all + li * 2 * c.ffn;
+        l.sd = x->sd_all + li * c.hidden;
+      }
     }
   }
 #undef AM
@@ -236,6 +267,19 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->best, c.max_batch);
   A(x->seen, (size_t)slots * c.vocab);
   A(x->penalty, 1);
+  x->mega_ok = c.hidden == 3072 && c.heads == 24 && c.kv_heads == 8 && c.head_dim == 128 &&
+               c.ffn == 8192;
+  if (x->mega_ok) {
+    x->mega_nsplit_cap = std::min(c.max_pos / MEGA_SPLIT, MEGA_MAX_SPLITS);
+    x->mega_sync_bytes = ((size_t)(c.layers * MEGA_SYNC_LAYER + 1) * 4 + 15) / 16 * 16;
+    A(x->mega_ws, NL * MEGA_WS_LAYER);
+    A(x->mega_part, NL * 8 * x->mega_nsplit_cap * MEGA_PART);
+    A(x->mega_sync, x->mega_sync_bytes / 4);
+    A(x->h_fin, c.hidden);
+    uint8_t* dm = nullptr;
+    A(dm, 128 * 1024);
+    x->mega_dummy = dm;
+  }
 #undef A
   if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
@@ -269,6 +313,13 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
     e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
   if (e == hipSuccess) e = gemv_prepare(std::max(std::max(c.hidden, c.ffn), c.heads * 128));
+  if (e == hipSuccess && x->mega_ok) {
+    e = hipMemset(x->mega_dummy, 0, 128 * 1024);
+    if (e == hipSuccess) e = hipMemset(x->mega_sync, 0, x->mega_sync_bytes);
+    int ok = 0;
+    if (e == hipSuccess) e = mega_resident(device, f8 ? 1 : 0, x->mega_ring, &ok);
+    x->mega_ok = ok != 0;
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
     g_err = std::string("init failed: ") + hipGetErrorString(e);
@@ -575,6 +626,42 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, hipStream_t
   return e;
 }
 
+// One-row step through the persistent kernel: memset of the hand-off words (a graph node),
+// the layers in one launch, then the lm_head / argmax and the commit as usual.
+static bool mega_eligible(const mx_llm* x, int n_rows, int max_len) {
+  return x->mega && x->mega_ok && n_rows == 1 && max_len <= x->mega_nsplit_cap * MEGA_SPLIT;
+}
+
+static hipError_t enqueue_decode_mega(mx_llm* x, hipStream_t st) {
+  const auto& c = x->c;
+  const bool f8 = c.wdtype == WT_FP8;
+  MegaArgs m{};
+  m.wqkv = x->wqkv_all; m.wo = x->wo_all; m.wgu = x->wgu_all; m.wd = x->wd_all;
+  m.sqkv = x->sqkv_all; m.so = x->so_all; m.sgu = x->sgu_all; m.sd = x->sd_all;
+  m.attn_norm = x->attn_norm_all; m.mlp_norm = x->mlp_norm_all;
+  m.rope_cos = x->rope_cos; m.rope_sin = x->rope_sin;
+  m.row_slot = x->row_slot; m.row_pos = x->row_pos;
+  m.kcache = x->kcache; m.vcache = x->vcache; m.kv_layer_elems = x->kv_layer_elems;
+  m.max_pos = c.max_pos; m.layers = c.layers; m.nsplit_cap = x->mega_nsplit_cap;
+  m.f8 = f8 ? 1 : 0; m.ring = x->mega_ring;
+  m.h_in = x->h_dec; m.h_out = x->h_fin; m.ws = x->mega_ws; m.part = x->mega_part;
+  m.sync = x->mega_sync; m.dummy = x->mega_dummy;
+  m.eps = c.eps; m.att_scale = 1.0f / sqrtf(128.0f);
+  m.trace = x->mega_trace;
+  hipError_t e = hipMemsetAsync(x->mega_sync, 0, x->mega_sync_bytes, st);
+  if (e == hipSuccess) e = launch_mega(m, st);
+  if (e == hipSuccess) e = enqueue_head(x, x->h_fin, x->row_slot, 1, x->best, st);
+  if (e == hipSuccess) {
+    CommitArgs cm{};
+    cm.best = x->best; cm.row_slot = x->row_slot; cm.row_pos = x->row_pos;
+    cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
+    cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
+    cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
+    e = launch_commit(cm, 1, st);
+  }
+  return e;
+}
+
 static int set_penalty(mx_llm* x, float p, hipStream_t st) {
   if (p != x->penalty_host) {
     MX_TRY(x, launch_set_scalar(x->penalty, p, st));
@@ -645,12 +732,15 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   const int S = 32 * (n_rows == 1 ? x->att_nw_b1 * x->att_cpw_b1
                                   : x->att_nw_batch * x->att_cpw_batch);
   const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
-  const int key = n_rows * 4096 + nsplit;
+  // the persistent one-row step reads the length on the device: one graph for every length
+  const bool mega = mega_eligible(x, n_rows, decode_max_len(x, n_rows));
+  const int key = mega ? -1 : n_rows * 4096 + nsplit;
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
     MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
-    hipError_t e = enqueue_decode(x, n_rows, nsplit * S, x->cap, nullptr);
+    hipError_t e = mega ? enqueue_decode_mega(x, x->cap)
+                        : enqueue_decode(x, n_rows, nsplit * S, x->cap, nullptr);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(x->cap, &g);
     MX_TRY(x, e);
@@ -843,11 +933,27 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
   } else if (k == "rows_kernel") {
-    if (value != 4 && value != 5) MX_FAIL(x, MX_ERR_ARG, "rows_kernel must be 4 or 5");
+    if (value != 4 && value != 5 && value != 7) MX_FAIL(x, MX_ERR_ARG, "rows_kernel must be 4, 5 or 7");
     x->rows_kernel = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
+  } else if (k == "mega") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "mega must be 0 or 1");
+    x->mega = value;
+  } else if (k == "mega_trace") {
+    if (value && !x->mega_trace)
+      MX_TRY(x, x->alloc(&x->mega_trace, (size_t)MEGA_BLOCKS * x->c.layers * MEGA_TRACE_EV));
+    if (!value) x->mega_trace = nullptr;
+  } else if (k == "mega_ring") {
+    if (value != 8 && value != 16 && value != 32 && value != 48)
+      MX_FAIL(x, MX_ERR_ARG, "mega_ring must be 8, 16, 32 or 48");
+    if (x->mega_ok) {
+      int ok = 0;
+      MX_TRY(x, mega_resident(x->device, x->c.wdtype == WT_FP8 ? 1 : 0, value, &ok));
+      if (!ok) MX_FAIL(x, MX_ERR_STATE, "mega_ring: launch would not be co-resident");
+    }
+    x->mega_ring = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
     if (value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
@@ -873,6 +979,29 @@ extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
 }
 
 extern "C" int32_t* mx_llm_history(mx_llm* x) { return x ? x->hist_host : nullptr; }
+
+extern "C" int64_t mx_llm_mega_trace(mx_llm* x, int64_t* host_out, int64_t n) {
+  if (!x || !host_out) return MX_ERR_ARG;
+  if (!x->mega_trace) MX_FAIL(x, MX_ERR_STATE, "mega_trace option not enabled");
+  const int64_t total = (int64_t)MEGA_BLOCKS * x->c.layers * MEGA_TRACE_EV;
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, hipDeviceSynchronize());
+  MX_TRY(x, hipMemcpy(host_out, x->mega_trace, (size_t)std::min(n, total) * 8,
+                      hipMemcpyDeviceToHost));
+  return std::min(n, total);
+}
+
+extern "C" int mx_llm_mega_info(mx_llm* x, int* eligible, int* status, void* stream) {
+  if (!x || !eligible || !status) return MX_ERR_ARG;
+  *eligible = x->mega && x->mega_ok ? 1 : 0;
+  *status = 0;
+  if (!x->mega_ok) return MX_OK;
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, hipStreamSynchronize((hipStream_t)stream));
+  MX_TRY(x, hipMemcpy(status, x->mega_sync + x->c.layers * MEGA_SYNC_LAYER, 4,
+                      hipMemcpyDeviceToHost));
+  return MX_OK;
+}
 
 extern "C" int mx_llm_debug_logits(mx_llm* x, int enable) {
   if (!x) return MX_ERR_ARG;

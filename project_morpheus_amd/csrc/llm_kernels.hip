@@ -848,7 +848,11 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
-    const hipError_t e = a.rows_kernel == 4 ? v4::launch_gemm_rows_v4(a, epi, norm, st)
+    if (a.rows_kernel == 7) {
+      const hipError_t e7 = launch_gemm_rows_v7(a, epi, norm, st);
+      if (e7 != hipErrorNotSupported) return e7;
+    }
+    const hipError_t e = a.rows_kernel != 5 ? v4::launch_gemm_rows_v4(a, epi, norm, st)
                                             : launch_gemm_rows(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
   }

@@ -117,6 +117,25 @@ class LlmEngine:
                                                     C.byref(us)))
         return us.value
 
+    def mega_info(self, stream) -> Dict[str, int]:
+        """Persistent one-row step: eligible (used by one-row decode graphs) and the give-up
+        status of its last launch (0 = every in-launch hand-off completed)."""
+        el, st = C.c_int(0), C.c_int(0)
+        self._check(self.lib.mx_llm_mega_info(self.h, C.byref(el), C.byref(st),
+                                              C.c_void_p(stream.cuda_stream)))
+        return {"eligible": el.value, "status": st.value}
+
+    def mega_trace(self):
+        """Event clocks of the last persistent step (option mega_trace=1):
+        int64 [256 blocks][layers][16] at 100 MHz."""
+        import numpy as np
+        n = 256 * self.cfg.layers * 16
+        out = np.zeros(n, dtype=np.int64)
+        got = self.lib.mx_llm_mega_trace(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), n)
+        if got < 0:
+            _lib.check(int(got), self.lib.mx_llm_last_error, self.h)
+        return out.reshape(256, self.cfg.layers, 16)
+
     def set_option(self, key: str, value: int) -> None:
         self._check(self.lib.mx_llm_set_option(self.h, key.encode(), int(value)))
 

@@ -24,11 +24,13 @@ def _cfg():
     return C.OrpheusConfig(hidden=1024, layers=2, heads=8, kv_heads=2, ffn=2048, vocab=1000)
 
 
-def _run(cfg, qw, prompts, steps):
+def _run(cfg, qw, prompts, steps, info=None, options=None):
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
     eng = LlmEngine(cfg, qw, device=0, max_slots=B, max_pos=512, max_batch=B, max_prefill=128,
                     wdtype="fp8")
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
     eng.enable_logits()
     st = torch.cuda.Stream()
     toks = [[] for _ in range(B)]
@@ -42,12 +44,14 @@ def _run(cfg, qw, prompts, steps):
         for r, p in enumerate(prompts):
             logits[r].append(eng.read_logits(r, st))
             toks[r].append(int(eng.hist[r, len(p) + k]))
+    if info is not None:
+        info.update(eng.mega_info(st))
     eng.close()
     return toks, logits
 
 
-def _check(cfg, qw, prompts, steps):
-    toks, logits = _run(cfg, qw, prompts, steps)
+def _check(cfg, qw, prompts, steps, info=None, options=None):
+    toks, logits = _run(cfg, qw, prompts, steps, info=info, options=options)
     rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
                      kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
     ref = L.LlamaRef(rc, dequantize_fp8(qw), max_pos=512)
@@ -80,3 +84,26 @@ def test_fp8_batched_6_rows():
     rng = np.random.default_rng(13)
     prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 4 + 3 * i)] for i in range(6)]
     assert _check(cfg, qw, prompts, 10) >= 0.8 * 60
+
+
+def test_fp8_single_stream_orpheus_width_persistent_step():
+    """e4m3 weights at Orpheus widths (2 layers), option mega=1: the one-row step runs as the persistent
+    launch (16 weights per 16-byte unit, v_cvt_pk_f32_fp8, per-row scales in the control
+    wave's epilogues); 120-id prompt + 20 steps: the context crosses 128 (two splits)."""
+    cfg = C.OrpheusConfig(layers=2)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=53), cfg)
+    rng = np.random.default_rng(14)
+    prompt = [int(x) for x in rng.integers(1000, 128000, 120)]
+    info = {}
+    assert _check(cfg, qw, [prompt], 20, info=info, options={"mega": 1}) >= 15
+    assert info == {"eligible": 1, "status": 0}
+
+
+def test_fp8_batched_orpheus_width_gen7():
+    """8 fp8 streams at Orpheus widths (configs[4] per GPU), option rows_kernel=7: generation-7 GEMM with e4m3
+    A-fragments (one 16-byte load = two k-steps, v_cvt_scalef32_pk_bf16_fp8)."""
+    cfg = C.OrpheusConfig(layers=2)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=54), cfg)
+    rng = np.random.default_rng(15)
+    prompts = [[int(x) for x in rng.integers(1000, 128000, 5 + 4 * i)] for i in range(8)]
+    assert _check(cfg, qw, prompts, 6, options={"rows_kernel": 7}) >= 0.8 * 8 * 6

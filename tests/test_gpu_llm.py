@@ -34,10 +34,12 @@ def _ref_cfg(c):
                        rope_theta=c.rope_theta, rope_scaling=c.rope_scaling)
 
 
-def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512):
+def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512, options=None, info=None):
     from project_morpheus_amd.engine import LlmEngine
     eng = LlmEngine(cfg, w, device=0, max_slots=2, max_pos=max_pos, max_batch=1,
                     max_prefill=256)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
     eng.enable_logits()
     st = torch.cuda.Stream()
     toks, logits = [], []
@@ -48,16 +50,18 @@ def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512):
             eng.decode(1, penalty, st)
         logits.append(eng.read_logits(0, st))
         toks.append(int(eng.hist[slot, len(prompt) + k]))
+    if info is not None:
+        info.update(eng.mega_info(st))
     eng.close()
     return toks, logits
 
 
-def _compare(cfg, w, prompt, steps, penalty=1.1):
+def _compare(cfg, w, prompt, steps, penalty=1.1, options=None, info=None):
     """Teacher-forced comparison: the oracle is fed the GPU's tokens, so every step's
     logits are compared; a token may differ from the oracle's own argmax only where the
     oracle's top-2 margin is below TIE_MARGIN (near-tie).  Returns the number of steps whose
     argmax agreed."""
-    g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, penalty)
+    g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, penalty, options=options, info=info)
     ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=512)
     r_toks, r_logits = L.greedy_generate(ref, prompt, steps, penalty, return_logits=True,
                                          forced=g_toks)
@@ -107,6 +111,52 @@ def test_decode_parity_orpheus_width_2_layers():
     assert _compare(cfg, w, prompt, 24) >= 20
 
 
+def _orpheus_prompt(n_text, seed):
+    return [128259, 128000] + [int(x) for x in np.random.default_rng(seed).integers(1000, 128000, n_text)] \
+        + [128009, 128260, 128261, 128257]
+
+
+def test_mega_step_is_used_and_completes():
+    """Option mega=1 at Orpheus widths: the one-row step runs as ONE persistent launch
+    (llm_mega.hip; off by default); its
+    in-launch hand-offs all completed (status 0) and it matches the oracle."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=5)
+    info = {}
+    assert _compare(cfg, w, _orpheus_prompt(12, 6), 20, options={"mega": 1}, info=info) >= 16
+    assert info == {"eligible": 1, "status": 0}
+
+
+def test_mega_three_layers_attention_splits():
+    """3 layers (two layer seams of the weight ring plus the tail), prompt of 230 ids and 60
+    steps: the context crosses 256, so the persistent step runs 2 then 3 attention splits per
+    kv head with the last-arriver merge, and the new position moves across split edges."""
+    cfg = C.OrpheusConfig(layers=3)
+    w = synthetic_llm_weights(cfg, seed=7)
+    info = {}
+    assert _compare(cfg, w, _orpheus_prompt(226, 8), 60, options={"mega": 1}, info=info) >= 45
+    assert info == {"eligible": 1, "status": 0}
+
+
+def test_mega_matches_multi_kernel_step():
+    """Persistent step vs the per-kernel step on the same weights and prompt: penalised logits
+    agree to the same tolerance the oracle comparison uses, token for token."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=9)
+    prompt = _orpheus_prompt(40, 10)
+    i1, i0 = {}, {}
+    t1, l1 = _run_gpu(cfg, w, prompt, 16, 1.1, options={"mega": 1}, info=i1)
+    t0, l0 = _run_gpu(cfg, w, prompt, 16, 1.1, options={"mega": 0}, info=i0)
+    assert i1["eligible"] == 1 and i1["status"] == 0 and i0["eligible"] == 0
+    for k in range(16):
+        np.testing.assert_allclose(l1[k], l0[k], atol=LOGIT_TOL, rtol=LOGIT_TOL,
+                                   err_msg=f"step {k}")
+        if t1[k] != t0[k]:
+            top2 = np.sort(l0[k])[-2:]
+            assert top2[1] - top2[0] < TIE_MARGIN
+            break  # histories diverge after a near-tie flip
+
+
 def test_bad_args_fail_loudly():
     from project_morpheus_amd import _lib
     from project_morpheus_amd.engine import LlmEngine
@@ -126,13 +176,15 @@ def test_bad_args_fail_loudly():
         LlmEngine(cfg, bad, max_slots=1, max_pos=128)   # incomplete weights
 
 
-def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None):
+def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=None):
     """Batched decode: every prompt on its own slot and decode row, all rows stepped together
     (the B >= 2 MFMA path); each row teacher-forced against its own oracle run."""
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
     eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=512, max_batch=max_batch or B,
                     max_prefill=256)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
     eng.enable_logits()
     st = torch.cuda.Stream()
     toks = [[] for _ in range(B)]
@@ -190,3 +242,25 @@ def test_batched_decode_orpheus_width_4_rows():
     prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 8 + 3 * i)]
                + [128009, 128260, 128261, 128257] for i in range(4)]
     assert _compare_rows(cfg, w, prompts, 10) >= 0.8 * 4 * 10
+
+
+def test_batched_decode_orpheus_width_20_rows_gen7():
+    """20 streams at Orpheus widths through the generation-7 multi-row GEMM (option
+    rows_kernel=7: one block per 16-row weight tile, K over its 8 / 16 waves, 32-row batch
+    tiles) for qkv / o / gate-up / down / lm_head; ragged prompts."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=21)
+    rng = np.random.default_rng(22)
+    prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 4 + 2 * i)]
+               + [128009, 128260, 128261, 128257] for i in range(20)]
+    assert _compare_rows(cfg, w, prompts, 6, options={"rows_kernel": 7}) >= 0.8 * 20 * 6
+
+
+def test_batched_decode_orpheus_width_gen4():
+    """The default multi-row generation (rows_kernel=4) at Orpheus widths, 6 rows."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=23)
+    rng = np.random.default_rng(24)
+    prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 6 + i)]
+               + [128009, 128260, 128261, 128257] for i in range(6)]
+    assert _compare_rows(cfg, w, prompts, 6, options={"rows_kernel": 4}) >= 0.8 * 6 * 6
