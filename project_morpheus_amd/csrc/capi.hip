@@ -115,11 +115,14 @@ struct mx_llm {
   float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
-  int att_cpw_batch = 1;        // option: same for multi-row (batched decode / prefill)
+  int att_cpw_batch = 4;        // option: same for multi-row (batched decode / prefill); 4
+                                // measured -14 % attention time at 32 rows, L ~600
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
   int rows_kernel = 4;               // option: multi-row GEMM generation (4 measured fastest; 7, 5)
+  int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
+  int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent single-stream step (llm_mega.hip): eligible shapes + co-residency checked at
   // create; option "mega" (default 0) picks it for one-row decode graphs
@@ -498,6 +501,8 @@ struct RowSet {
 static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_dbg = x->rows_dbg;
   g.rows_kernel = x->rows_kernel;
+  g.rows_pw = x->rows_pw;
+  g.rows_target = x->rows_target;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -938,6 +943,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
+  } else if (k == "rows_pw") {
+    if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw must be 1 or 2");
+    x->rows_pw = value;
+  } else if (k == "rows_target") {
+    if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
+    x->rows_target = value;
   } else if (k == "mega") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "mega must be 0 or 1");
     x->mega = value;

@@ -144,6 +144,18 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
   }
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte write-through (sc1) store / load of a partial-tile quad (MI355X_MICROARCH.md
+// "Valid forms" row 1 with 16-B accesses)
+__device__ __forceinline__ void st4_wt(float* base, size_t idx, const f32x4& v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(idx * 4), 0, 16);
+}
+__device__ __forceinline__ f32x4 ld4_wt(const float* base, size_t idx) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -165,9 +177,13 @@ __device__ __forceinline__ float ld_wt(const float* p) {
 // registers by v_cvt_scalef32_pk_bf16_fp8, exact) with a per-row scale in the epilogue.  A
 // lane's 16 bytes hold k = 64 P + 16 g .. +15, so k-step 2P + h contracts k = 64 P + 16 g +
 // 8 h + j, and the activation fragments are staged in that (consistent) k order.
-template <int MT, int NT, int EPI, bool NORM, int SUB, bool F8>
+// PW: weight prefetch distance in sub-chunks (1 = the original double buffer); with PW > 1 the
+// activation pieces run DX = 2 sub-chunks ahead and are issued BEFORE each sub-chunk's
+// weights, so the in-order vmcnt wait that stages X(s+1) only drains weights already needed.
+template <int MT, int NT, int EPI, bool NORM, int SUB, bool F8, int PW = 1>
 __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
   constexpr int NP = 3, ST = 4;             // activation parts; k-steps per sub-chunk
+  constexpr int DX = PW > 1 ? 2 : 1, NBX = DX + 1, NBW = PW + 1;  // prefetch distances, buffers
   constexpr int ITEMS = (NT * 16 * 16) / 512 > 0 ? (NT * 16 * 16) / 512 : 1;  // X pieces/thread
   constexpr int WSLAB = MT * NT * 4 * 64;   // floats per wave partial
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -203,9 +219,9 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
 #pragma unroll
   for (int it = 0; it < ITEMS; ++it) ssp[it] = 0.f;
 
-  float4 xr[2][ITEMS][2], nr[2][ITEMS][2];
+  float4 xr[NBX][ITEMS][2], nr[NBX][ITEMS][2];
   constexpr int WL = F8 ? ST / 2 : ST;      // 16-byte weight loads per row per sub-chunk
-  uint4 wv[2][WL][MT];
+  uint4 wv[NBW][WL][MT];
   auto load_x = [&](int sub, int buf) {
     const int k = kr0 + 128 * sub;
 #pragma unroll
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
                                                  __builtin_bit_cast(uint32_t, e2),
                                                  __builtin_bit_cast(uint32_t, e3)));
   };
-  auto stage_x = [&](int buf) {
+  auto stage_x2 = [&](int buf, int lb) {
     if (!xact) return;
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
@@ -261,9 +277,10 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
       const int gq = F8 ? (j & 7) >> 1 : j & 3;
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        xs[buf][p][b >> 4][st][gq * 16 + (b & 15)] = __builtin_bit_cast(uint4, pf[p]);
+        xs[lb][p][b >> 4][st][gq * 16 + (b & 15)] = __builtin_bit_cast(uint4, pf[p]);
     }
   };
+  auto stage_x = [&](int buf) { stage_x2(buf, 0); };
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -271,17 +288,20 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_x(0, 0);
-  load_w(0, 0);
+#pragma unroll
+  for (int d = 0; d < DX; ++d)
+    if (d < SUB) load_x(d, d % NBX);
+#pragma unroll
+  for (int d = 0; d < PW; ++d)
+    if (d < SUB) load_w(d, d % NBW);
   stage_x(0);
   __syncthreads();
 #pragma unroll
   for (int sub = 0; sub < SUB; ++sub) {
-    const int cur = sub & 1, nxt = cur ^ 1;
-    if (sub + 1 < SUB) {
-      load_x(sub + 1, nxt);
-      load_w(sub + 1, nxt);
-    }
+    const int cur = sub & 1, nxt = cur ^ 1;  // LDS buffers
+    if (sub + DX < SUB) load_x(sub + DX, (sub + DX) % NBX);
+    if (sub + PW < SUB) load_w(sub + PW, (sub + PW) % NBW);
+    const int wb = sub % NBW;
 #pragma unroll
     for (int st = 0; st < ST; ++st) {
 #pragma unroll
@@ -291,12 +311,12 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
           const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xs[cur][p][nt][st][lane]);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(cur, st, mt), xb8,
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(wb, st, mt), xb8,
                                                                   acc[mt][nt], 0, 0, 0);
         }
       }
     }
-    if (sub + 1 < SUB) stage_x(nxt);
+    if (sub + 1 < SUB) stage_x2((sub + 1) % NBX, nxt);
     __syncthreads();
   }
   // per-row sum of squares of this K range: the 16 threads of a row are 16 adjacent lanes
@@ -321,13 +341,14 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
     const size_t slab_floats = 8 * (size_t)WSLAB + 16 * NT;
     float* base = a.ws + tile * nkc * slab_floats;
     float* mine = base + (size_t)kc * slab_floats;
+    // lane-major partial: a lane's MT x NT quads are contiguous (16-byte sc1 accesses); the
+    // buffer descriptor stays block-uniform (a per-lane base would be a waterfall loop)
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const size_t lofs = (size_t)wu * WSLAB + (size_t)lane * (4 * MT * NT);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          st_wt(mine + (size_t)w * WSLAB + ((mt * NT + nt) * 4 + i) * 64 + lane, acc[mt][nt][i]);
+      for (int nt = 0; nt < NT; ++nt) st4_wt(mine, lofs + (mt * NT + nt) * 4, acc[mt][nt]);
     if (NORM && tid < 16 * NT) st_wt(mine + 8 * (size_t)WSLAB + tid, ssrow[tid]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -346,18 +367,35 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
       for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) ss[nt] = 0.f;
-    for (int q = 0; q < nkc; ++q) {
-      const float* src = base + (size_t)q * slab_floats;
+    // the K ranges' partials, four ranges' loads in flight at a time, summed in range order
+    for (int q0 = 0; q0 < nkc; q0 += 4) {
+      f32x4 t[4][MT][NT];
+      float sq[4][NT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int j = 0; j < 4; ++j) {
+        const float* src = base + (size_t)min(q0 + j, nkc - 1) * slab_floats;
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[mt][nt][i] += ld_wt(src + (size_t)w * WSLAB + ((mt * NT + nt) * 4 + i) * 64 + lane);
-      if (NORM) {
+          for (int nt = 0; nt < NT; ++nt) t[j][mt][nt] = ld4_wt(src, lofs + (mt * NT + nt) * 4);
+        if (NORM) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) ss[nt] += ld_wt(src + 8 * (size_t)WSLAB + 16 * nt + c);
+          for (int nt = 0; nt < NT; ++nt) sq[j][nt] = ld_wt(src + 8 * (size_t)WSLAB + 16 * nt + c);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (q0 + j >= nkc) break;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[mt][nt][i] += t[j][mt][nt][i];
+        if (NORM) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) ss[nt] += sq[j][nt];
+        }
       }
     }
   }
@@ -370,17 +408,17 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
 
 // K ranges per launch: enough blocks to fill the chip without inflating the partial-tile
 // traffic (each range adds R x N x 4 bytes of write-through partials).
-static int rows_nkc(int N, int K, int R, int MT, int NT) {
+static int rows_nkc(int N, int K, int R, int MT, int NT, int target = 384) {
   const int subs = K / 128;
   const int tiles = ((N + 128 * MT - 1) / (128 * MT)) * ((R + 16 * NT - 1) / (16 * NT));
   int nkc = 1;
-  while (tiles * nkc < 384 && subs % (2 * nkc) == 0 && subs / (2 * nkc) >= 2) nkc *= 2;
-  while (tiles * nkc < 384 && subs % (3 * nkc) == 0 && subs / (3 * nkc) >= 2) nkc *= 3;
+  while (tiles * nkc < target && subs % (2 * nkc) == 0 && subs / (2 * nkc) >= 2) nkc *= 2;
+  while (tiles * nkc < target && subs % (3 * nkc) == 0 && subs / (3 * nkc) >= 2) nkc *= 3;
   return nkc;
 }
 
-template <int MT, int NT, int EPI, bool NORM, int SUB>
-static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
+template <int MT, int NT, int EPI, bool NORM, int SUB, int PW>
+static hipError_t launch_rows_pw(const GemvArgs& a, int nkc, hipStream_t st) {
   if (a.wdtype == WT_FP8 && a.K % 128) return hipErrorNotSupported;
   const int tiles_n = (a.N + 128 * MT - 1) / (128 * MT), tiles_r = (a.R + 16 * NT - 1) / (16 * NT);
   if (nkc > 1) {
@@ -389,17 +427,33 @@ static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
       return hipErrorInvalidValue;
   }
   const dim3 grid(tiles_n, nkc, tiles_r);
-  if (a.wdtype == WT_FP8)
-    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, true>), grid, dim3(512), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, false>), grid, dim3(512), 0, st, a);
+  if (a.wdtype == WT_FP8) {
+    if constexpr (PW == 1)
+      hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, true, 1>), grid, dim3(512), 0, st, a);
+    else
+      return hipErrorNotSupported;
+  } else {
+    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, false, PW>), grid, dim3(512), 0, st, a);
+  }
   return hipGetLastError();
+}
+
+// Prefetch distance 2 (bf16): measured 97.3 vs 103.5 us per layer of projections at 32 rows,
+// neutral at 8 rows; distance 3 was slower (scripts/gpu_pw.sh).  fp8 keeps distance 1.
+template <int MT, int NT, int EPI, bool NORM, int SUB>
+static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
+  if (a.rows_pw == 2 && SUB > 1 && a.wdtype != WT_FP8)
+    return launch_rows_pw<MT, NT, EPI, NORM, SUB, 2>(a, nkc, st);
+  return launch_rows_pw<MT, NT, EPI, NORM, SUB, 1>(a, nkc, st);
 }
 
 template <int MT, int NT, int EPI, bool NORM>
 static hipError_t launch_rows_k(const GemvArgs& a, hipStream_t st) {
   if (a.K % 128) return hipErrorNotSupported;
-  const int nkc = rows_nkc(a.N, a.K, a.R, MT, NT);
+  // K-range split target (blocks): measured at 8 and 32 rows (scripts/gpu_target.sh) the qkv
+  // projection is fastest aiming at 128 blocks, the others at 192 (384 was the old default)
+  const int target = a.rows_target > 0 ? a.rows_target : (EPI == EPI_QKV ? 128 : 192);
+  const int nkc = rows_nkc(a.N, a.K, a.R, MT, NT, target);
   switch (a.K / 128 / nkc) {
     case 1: return launch_rows_sub<MT, NT, EPI, NORM, 1>(a, nkc, st);
     case 2: return launch_rows_sub<MT, NT, EPI, NORM, 2>(a, nkc, st);

@@ -13,17 +13,27 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1)
+    ap.add_argument("--kinds", default="qkv,o_proj,gate_up,down")
+    ap.add_argument("--options", default="", help="k=v,k=v set_option knobs")
+    args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
     from project_morpheus_amd.engine import LlmEngine
     from project_morpheus_amd.weights import synthetic_llm_weights
     cfg = C.OrpheusConfig()
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
-    llm = LlmEngine(cfg, w, device=0, max_slots=1, max_pos=2048, max_batch=1, max_prefill=64)
+    R = args.rows
+    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=64)
     del w
     torch.cuda.empty_cache()
-    for kind in ("qkv", "o_proj", "gate_up", "down"):
-        us, nb = llm.bench_gemv(kind, reps=1)
+    for kv in filter(None, args.options.split(",")):
+        k, v = kv.split("=")
+        llm.set_option(k, int(v))
+    for kind in args.kinds.split(","):
+        us, nb = llm.bench_gemv(kind, reps=1, n_rows=R)
         print(f"{kind}: {us:.2f} us/launch, {nb:.0f} weight bytes/launch", flush=True)
 
 
