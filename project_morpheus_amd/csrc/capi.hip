@@ -115,8 +115,8 @@ struct mx_llm {
   float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
-  int att_cpw_batch = 4;        // option: same for multi-row (batched decode / prefill); 4
-                                // measured -14 % attention time at 32 rows, L ~600
+  int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
+                                // auto (att_cpw_auto): measured -14 % attention at 32 rows
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
@@ -490,12 +490,28 @@ extern "C" int mx_llm_finalize(mx_llm* x) {
 }
 
 // ---- one forward over `R` rows (decode rows or prefill rows) -------------------------
+// Multi-row attention: 32-position chunks per wave.  Longer splits avoid the cross-block merge
+// but shrink the grid; take the longest split (4, 2 chunks) that still gives >= 256 blocks
+// (one per CU), else 1.  At 32 rows and L ~600 this picks 4 (measured -14 % attention time vs
+// 1); at 8 rows it keeps 1 (4 would leave 64 blocks).
+static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
+  if (R == 1) return x->att_cpw_b1;
+  if (x->att_cpw_batch > 0) return x->att_cpw_batch;
+  for (int cpw : {4, 2}) {
+    const int S = 32 * x->att_nw_batch * cpw;
+    const long blocks = (long)((max_len + S - 1) / S) * x->c.kv_heads * R;
+    if (blocks >= 256) return cpw;
+  }
+  return 1;
+}
+
 struct RowSet {
   float* h;
   const int32_t* slot;
   const int32_t* pos;
   int R;
   int max_len;  // upper bound of any row's position + 1 (sizes the attention grid)
+  int cpw;      // attention chunks per wave (att_cpw_auto)
 };
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
@@ -552,7 +568,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.Q = x->q; at.kcache = kc; at.vcache = vc; at.row_slot = rs.slot; at.row_pos = rs.pos;
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
     at.scale = 1.0f / sqrtf(128.0f);
-    at.cpw = rs.R == 1 ? x->att_cpw_b1 : x->att_cpw_batch;
+    at.cpw = rs.cpw;
     at.nw = rs.R == 1 ? x->att_nw_b1 : x->att_nw_batch;
     at.split_stride = c.max_pos / ATT_S_MIN;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
@@ -611,9 +627,10 @@ static int decode_max_len(const mx_llm* x, int n_rows) {
   return m;
 }
 
-static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, hipStream_t st, Prof* prof) {
+static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hipStream_t st,
+                                 Prof* prof) {
   const auto& c = x->c;
-  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len};
+  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw};
   hipError_t e = enqueue_layers(x, rs, st, prof);
   PROF_BEGIN(PK_HEAD);
   if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, n_rows, x->best, st);
@@ -693,7 +710,7 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, launch_set_rows(x->pre_slot, x->pre_pos, n, slot, 0, st));
   MX_TRY(x, launch_embed_rows(x->pre_ids, n, slot, x->embed, c.hidden, c.vocab, x->seen,
                               x->h_pre, st));
-  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n};
+  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n, att_cpw_auto(x, n, n)};
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
   MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1), 1,
@@ -734,18 +751,19 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
-  const int S = 32 * (n_rows == 1 ? x->att_nw_b1 * x->att_cpw_b1
-                                  : x->att_nw_batch * x->att_cpw_batch);
+  const int cpw = att_cpw_auto(x, n_rows, decode_max_len(x, n_rows));
+  const int S = 32 * cpw * (n_rows == 1 ? x->att_nw_b1 : x->att_nw_batch);
   const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
   // the persistent one-row step reads the length on the device: one graph for every length
   const bool mega = mega_eligible(x, n_rows, decode_max_len(x, n_rows));
-  const int key = mega ? -1 : n_rows * 4096 + nsplit;
+  // (the chunk count is part of the key: one nsplit can come from two chunk counts)
+  const int key = mega ? -1 : (n_rows * 8 + cpw) * 4096 + nsplit;
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
     MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
     hipError_t e = mega ? enqueue_decode_mega(x, x->cap)
-                        : enqueue_decode(x, n_rows, nsplit * S, x->cap, nullptr);
+                        : enqueue_decode(x, n_rows, nsplit * S, cpw, x->cap, nullptr);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(x->cap, &g);
     MX_TRY(x, e);
@@ -770,7 +788,8 @@ extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, float penalty, void
   if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   Prof prof;
-  hipError_t e = enqueue_decode(x, n_rows, decode_max_len(x, n_rows), st, &prof);
+  const int ml = decode_max_len(x, n_rows);
+  hipError_t e = enqueue_decode(x, n_rows, ml, att_cpw_auto(x, n_rows, ml), st, &prof);
   mirror_step(x, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   for (auto& p : prof.ev) {
@@ -966,7 +985,8 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     }
     x->mega_ring = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
-    if (value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4");
+    if (value != 1 && value != 2 && value != 4 && !(value == 0 && k == "att_cpw_batch"))
+      MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4 (att_cpw_batch also 0 = auto)");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
   } else {
     MX_FAIL(x, MX_ERR_ARG, "unknown option " + k);

@@ -282,11 +282,15 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
   };
   auto stage_x = [&](int buf) { stage_x2(buf, 0); };
 
-  f32x4 acc[MT][NT];
+  // one accumulator per activation part: NP x NT x MT independent MFMA chains, so consecutive
+  // MFMAs never wait on each other's result (SQ_WAIT_INST_ANY was 38 % of wave cycles)
+  f32x4 pacc[NP][MT][NT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) pacc[p][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int d = 0; d < DX; ++d)
@@ -304,21 +308,29 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemvArgs a) {
     const int wb = sub % NBW;
 #pragma unroll
     for (int st = 0; st < ST; ++st) {
+      bf16x8 af[MT];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
+      for (int mt = 0; mt < MT; ++mt) af[mt] = afrag(wb, st, mt);
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
+      for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
           const bf16x8 xb8 = __builtin_bit_cast(bf16x8, xs[cur][p][nt][st][lane]);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag(wb, st, mt), xb8,
-                                                                  acc[mt][nt], 0, 0, 0);
+            pacc[p][mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], xb8,
+                                                                      pacc[p][mt][nt], 0, 0, 0);
         }
       }
     }
     if (sub + 1 < SUB) stage_x2((sub + 1) % NBX, nxt);
     __syncthreads();
   }
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (pacc[0][mt][nt] + pacc[1][mt][nt]) + pacc[2][mt][nt];
   // per-row sum of squares of this K range: the 16 threads of a row are 16 adjacent lanes
   if (NORM) {
 #pragma unroll
