@@ -122,6 +122,7 @@ struct mx_llm {
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
   int rows_kernel = 4;               // option: multi-row GEMM generation (4 measured fastest; 7, 5)
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
+  int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent single-stream step (llm_mega.hip): eligible shapes + co-residency checked at
@@ -518,6 +519,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_dbg = x->rows_dbg;
   g.rows_kernel = x->rows_kernel;
   g.rows_pw = x->rows_pw;
+  g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
@@ -962,9 +964,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
-  } else if (k == "rows_pw") {
-    if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw must be 1 or 2");
-    x->rows_pw = value;
+  } else if (k == "rows_pw" || k == "rows_pw_f8") {
+    if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw / rows_pw_f8 must be 1 or 2");
+    (k == "rows_pw" ? x->rows_pw : x->rows_pw_f8) = value;
   } else if (k == "rows_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;

@@ -440,22 +440,24 @@ static hipError_t launch_rows_pw(const GemvArgs& a, int nkc, hipStream_t st) {
   }
   const dim3 grid(tiles_n, nkc, tiles_r);
   if (a.wdtype == WT_FP8) {
-    if constexpr (PW == 1)
-      hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, true, 1>), grid, dim3(512), 0, st, a);
+    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, true, PW>), grid, dim3(512), 0, st, a);
+  } else {
+    if constexpr (PW <= 2)
+      hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, false, PW>), grid, dim3(512), 0, st, a);
     else
       return hipErrorNotSupported;
-  } else {
-    hipLaunchKernelGGL((gemm_rows_kernel<MT, NT, EPI, NORM, SUB, false, PW>), grid, dim3(512), 0, st, a);
   }
   return hipGetLastError();
 }
 
 // Prefetch distance 2 (bf16): measured 97.3 vs 103.5 us per layer of projections at 32 rows,
-// neutral at 8 rows; distance 3 was slower (scripts/gpu_pw.sh).  fp8 keeps distance 1.
+// neutral at 8 rows; distance 3 was slower (scripts/gpu_pw.sh).  e4m3 weights (half the bytes
+// per sub-chunk): distance 2 measured 53.6 vs 66.3 us per layer at 8 rows, 3 no better
+// (scripts/gpu_f8pw.sh).
 template <int MT, int NT, int EPI, bool NORM, int SUB>
 static hipError_t launch_rows_sub(const GemvArgs& a, int nkc, hipStream_t st) {
-  if (a.rows_pw == 2 && SUB > 1 && a.wdtype != WT_FP8)
-    return launch_rows_pw<MT, NT, EPI, NORM, SUB, 2>(a, nkc, st);
+  const int pw = a.wdtype == WT_FP8 ? a.rows_pw_f8 : a.rows_pw;
+  if (pw >= 2 && SUB > 1) return launch_rows_pw<MT, NT, EPI, NORM, SUB, 2>(a, nkc, st);
   return launch_rows_pw<MT, NT, EPI, NORM, SUB, 1>(a, nkc, st);
 }
 
