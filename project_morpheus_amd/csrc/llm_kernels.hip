@@ -453,8 +453,8 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
 }
 
 // One block = NW waves over S = 32 NW CPW positions of one (row, kv head); wave w takes the
-// CPW consecutive 32-position chunks starting at 32 (w CPW), with the next chunk's K / V^T
-// loads in flight under the current chunk's MFMAs and softmax.  NW = 8, CPW = 4 covers
+// 32-position chunks w, w + NW, ... (CPW of them), with the next chunk's K / V^T loads in
+// flight under the current chunk's MFMAs and softmax.  NW = 8, CPW = 4 covers
 // 1,024 positions in one block, so a single-row step up to that length needs no split merge.
 template <int GRP, int CPW, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
@@ -487,7 +487,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
     for (int t = 0; t < 8; ++t)
       vf[b][t] = *reinterpret_cast<const uint4*>(VT + (size_t)(16 * t + c) * a.max_pos + base + 8 * g);
   };
-  const int base0 = split * S + wid * CPW * 32;
+  // chunks are dealt round-robin over the waves (wave w: chunks w, w + NW, ...), so a split
+  // longer than the context still keeps every wave busy with ~equal work
+  const int base0 = split * S + wid * 32;
   if (base0 < L) load_kv(base0, 0);
 
   // Q^T fragments: lane (col c = head, group g) holds q[c][32 s + 8 g + j], 3 bf16 parts
@@ -517,9 +519,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
 #pragma unroll
   for (int ch = 0; ch < CPW; ++ch) {
     const int cb = ch & 1;
-    const int base = base0 + ch * 32;
+    const int base = base0 + ch * 32 * NW;
     if (base >= L) break;  // wave-uniform
-    if (ch + 1 < CPW && base + 32 < L) load_kv(base + 32, cb ^ 1);
+    if (ch + 1 < CPW && base + 32 * NW < L) load_kv(base + 32 * NW, cb ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     // scores
     f32x4 sc[2];
