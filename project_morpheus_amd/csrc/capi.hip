@@ -124,6 +124,7 @@ struct mx_llm {
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
+  int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent single-stream step (llm_mega.hip): eligible shapes + co-residency checked at
   // create; option "mega" (default 0) picks it for one-row decode graphs
@@ -521,6 +522,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_pw = x->rows_pw;
   g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
+  g.rows_nt_max = x->rows_nt_max;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -967,6 +969,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_pw" || k == "rows_pw_f8") {
     if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw / rows_pw_f8 must be 1 or 2");
     (k == "rows_pw" ? x->rows_pw : x->rows_pw_f8) = value;
+  } else if (k == "rows_nt_max") {
+    if (value != 0 && value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rows_nt_max must be 0, 1, 2 or 4");
+    x->rows_nt_max = value;
   } else if (k == "rows_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;

@@ -22,6 +22,8 @@
 #include "mx_common.h"
 #include "mx_llm_kernels.h"
 
+#include <algorithm>
+
 namespace mx {
 namespace v4 {
 
@@ -482,26 +484,35 @@ static hipError_t launch_rows_k(const GemvArgs& a, hipStream_t st) {
   }
 }
 
-static void rows_tiles(int epi, int R, int* mt, int* nt) {
+// Batch tile: 16 NT rows (nt_max caps it: option rows_nt_max).  Measured at 32 rows: a 16-row
+// cap is slower (102.7 vs 87.9 us per layer of projections), and 32 weight rows per wave
+// (one staged activation sub-chunk feeding twice the weights) far slower (141.7 us: half the
+// tiles leave CUs idle), so the weight tile stays 16 rows per wave.
+static void rows_tiles(int epi, int R, int* mt, int* nt, int nt_max = 4) {
   *nt = R <= 16 ? 1 : R <= 32 ? 2 : 4;
+  if (nt_max > 0 && *nt > nt_max) *nt = nt_max;
   *mt = 1;
 }
 
 // Workspace (floats) and tickets a launch of this shape needs (0 when K is one range).
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets) {
-  int mt, nt;
-  rows_tiles(epi, R, &mt, &nt);
-  const int nkc = K % 128 ? 1 : rows_nkc(N, K, R, mt, nt);
-  const size_t tn = (N + 128 * mt - 1) / (128 * mt), tr = (R + 16 * nt - 1) / (16 * nt);
-  *ws_floats = nkc > 1 ? tn * tr * nkc * (8 * (size_t)mt * nt * 4 * 64 + 16 * nt) : 0;
-  *tickets = tn * tr;
+  *ws_floats = 0;
+  *tickets = 0;
+  for (int cap : {1, 2, 4}) {  // every batch-tile cap option rows_nt_max may pick
+    int mt, nt;
+    rows_tiles(epi, R, &mt, &nt, cap);
+    const int nkc = K % 128 ? 1 : rows_nkc(N, K, R, mt, nt);
+    const size_t tn = (N + 128 * mt - 1) / (128 * mt), tr = (R + 16 * nt - 1) / (16 * nt);
+    *ws_floats = std::max(*ws_floats, nkc > 1 ? tn * tr * nkc * (8 * (size_t)mt * nt * 4 * 64 + 16 * nt) : (size_t)0);
+    *tickets = std::max(*tickets, tn * tr);
+  }
 }
 
 // R >= 2 rows.  Returns hipErrorNotSupported for shapes the kernel does not cover.
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   if (a.R < 1) return hipErrorNotSupported;
   int mt, nt;
-  rows_tiles(epi, a.R, &mt, &nt);
+  rows_tiles(epi, a.R, &mt, &nt, a.rows_nt_max);
 #define MX_R(EPI_, NORM_)                                                                 \
   if (epi == EPI_ && norm == NORM_) {                                                     \
     if (nt == 1) return launch_rows_k<1, 1, EPI_, NORM_>(a, st);                          \

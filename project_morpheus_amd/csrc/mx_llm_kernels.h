@@ -37,7 +37,8 @@ struct GemvArgs {
   int rows_npart;          // R >= 2 kernel: activation bf16 parts (2 or 3; 0 = 3)
   int rows_pw;             // generation 4: weight prefetch distance in sub-chunks (1, 2; 0 = 1)
   int rows_pw_f8;          // the same for e4m3 weights
-  int rows_target;         // generation 4: blocks the K-range split aims for (0 = 384)
+  int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
+  int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_kernel;         // R >= 2 kernel generation: 4 (default), 7 (falls back to 4 outside its shapes), 5
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
