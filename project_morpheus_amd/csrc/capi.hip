@@ -276,7 +276,7 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
                c.ffn == 8192;
   if (x->mega_ok) {
     x->mega_nsplit_cap = std::min(c.max_pos / MEGA_SPLIT, MEGA_MAX_SPLITS);
-    x->mega_sync_bytes = ((size_t)(c.layers * MEGA_SYNC_LAYER + 1) * 4 + 15) / 16 * 16;
+    x->mega_sync_bytes = (mega_sync_ints(c.layers) + mega_flag_ints(c.layers)) * 4;
     A(x->mega_ws, NL * MEGA_WS_LAYER);
     A(x->mega_part, NL * 8 * x->mega_nsplit_cap * MEGA_PART);
     A(x->mega_sync, x->mega_sync_bytes / 4);
@@ -672,6 +672,7 @@ static hipError_t enqueue_decode_mega(mx_llm* x, hipStream_t st) {
   m.f8 = f8 ? 1 : 0; m.ring = x->mega_ring;
   m.h_in = x->h_dec; m.h_out = x->h_fin; m.ws = x->mega_ws; m.part = x->mega_part;
   m.sync = x->mega_sync; m.dummy = x->mega_dummy;
+  m.flags = x->mega_sync + mega_sync_ints(c.layers);
   m.eps = c.eps; m.att_scale = 1.0f / sqrtf(128.0f);
   m.trace = x->mega_trace;
   hipError_t e = hipMemsetAsync(x->mega_sync, 0, x->mega_sync_bytes, st);

@@ -111,6 +111,30 @@ __device__ __forceinline__ void wait_ge(int* p, int target, int* status, int cod
   if ((threadIdx.x & 63) == 0)
     __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Per-block arrival flags of one grid seam: block b stores flags[b] = 1 (sc1, after its drain);
+// a consumer polls all 256 with ONE 16-byte sc1 load per lane and a wave vote.  No shared
+// counter line: 256 same-line atomic arrivals serialise (MI355X_MICROARCH.md, one-row
+// contention), which the event trace showed as ~7 us per seam.
+__device__ __forceinline__ void set_flag(int* f) {
+  drain();
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_flags(const int* f, int* status, int code, bool& dead) {
+  if (dead) return;
+  const int lane = threadIdx.x & 63;
+  for (int it = 0; it < SPIN_MAX; ++it) {
+    const float4 v = ld4_sc1(reinterpret_cast<const float*>(f), lane);  // flags 4 lane .. 4 lane + 3
+    const bool ok = __float_as_int(v.x) && __float_as_int(v.y) && __float_as_int(v.z) &&
+                    __float_as_int(v.w);
+    if (__all(ok)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  dead = true;
+  if (lane == 0) __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void signal(int* p) {
   drain();  // every sc1 store of this wave has left the CU before the count moves
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -597,10 +621,10 @@ __global__ __launch_bounds__(NTH, 1) void mega_kernel(MegaArgs a) {
           vc[(size_t)(within + 1) * a.max_pos + pos] = v2;
         }
       }
-      signal(sync + MEGA_SYNC_Q);
+      set_flag(a.flags + (l * 4 + 0) * NB + b);
       MEGA_EV(l, 1);
       if (att_blk) {
-        wait_ge(sync + MEGA_SYNC_Q, NB, status, 1, dead);
+        wait_flags(a.flags + (l * 4 + 0) * NB, status, 1, dead);
         MEGA_EV(l, 2);
         attention(sm, a, l, kvh, split, nsplit, L, qkv, lane, dead);
         MEGA_EV(l, 3);
@@ -622,8 +646,8 @@ __global__ __launch_bounds__(NTH, 1) void mega_kernel(MegaArgs a) {
         hres += y;
         st_sc1(ws + MEGA_OFF_HA + n, hres);
       }
-      signal(sync + MEGA_SYNC_O);
-      wait_ge(sync + MEGA_SYNC_O, NB, status, 3, dead);
+      set_flag(a.flags + (l * 4 + 1) * NB + b);
+      wait_flags(a.flags + (l * 4 + 1) * NB, status, 3, dead);
       MEGA_EV(l, 7);
       ssq = stage_x<F8, H>(sm, ws + MEGA_OFF_HA, a.mlp_norm + (size_t)l * H, lane);
     }
@@ -649,8 +673,8 @@ __global__ __launch_bounds__(NTH, 1) void mega_kernel(MegaArgs a) {
         }
         st_sc1(ws + MEGA_OFF_ACT + (n0 >> 1), gt / (1.0f + expf(-gt)) * up);
       }
-      signal(sync + MEGA_SYNC_G);
-      wait_ge(sync + MEGA_SYNC_G, NB, status, 4, dead);
+      set_flag(a.flags + (l * 4 + 2) * NB + b);
+      wait_flags(a.flags + (l * 4 + 2) * NB, status, 4, dead);
       MEGA_EV(l, 11);
       stage_x<F8, FF>(sm, ws + MEGA_OFF_ACT, nullptr, lane);
     }
@@ -668,9 +692,9 @@ __global__ __launch_bounds__(NTH, 1) void mega_kernel(MegaArgs a) {
         hres += y;
         st_sc1(hout + n, hres);
       }
-      signal(sync + MEGA_SYNC_D);
+      set_flag(a.flags + (l * 4 + 3) * NB + b);
       if (!last) {
-        wait_ge(sync + MEGA_SYNC_D, NB, status, 5, dead);
+        wait_flags(a.flags + (l * 4 + 3) * NB, status, 5, dead);
         MEGA_EV(l, 14);
         ssq = stage_x<F8, H>(sm, hout, a.attn_norm + (size_t)(l + 1) * H, lane);
       }

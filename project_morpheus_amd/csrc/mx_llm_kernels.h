@@ -106,6 +106,9 @@ constexpr int MEGA_SYNC_Q = 0, MEGA_SYNC_O = 1, MEGA_SYNC_G = 2, MEGA_SYNC_D = 3
 constexpr int MEGA_SYNC_TICK = 4;    // [8] split arrival tickets per kv head
 constexpr int MEGA_SYNC_DONE = 12;   // kv heads whose attention output is published
 constexpr int MEGA_SYNC_LAYER = 16;  // + one status word after the last layer (0 = ok)
+// sync words (+ status, padded to 16 B) are followed by the per-block seam flags
+inline size_t mega_sync_ints(int layers) { return ((size_t)layers * MEGA_SYNC_LAYER + 1 + 3) / 4 * 4; }
+inline size_t mega_flag_ints(int layers) { return (size_t)layers * 4 * MEGA_BLOCKS; }
 
 struct MegaArgs {
   const void *wqkv, *wo, *wgu, *wd;  // [layers][packed rows][K] contiguous (bf16 or e4m3)
@@ -122,6 +125,7 @@ struct MegaArgs {
   float* ws;                         // [layers][MEGA_WS_LAYER]
   float* part;                       // [layers][8][nsplit_cap][MEGA_PART]
   int* sync;                         // [layers][MEGA_SYNC_LAYER] + status
+  int* flags;                        // [layers][4 seams][256 blocks] arrival flags (same memset)
   const void* dummy;                 // >= 128 KB of zeros: the ring's loads past the last layer
   float eps, att_scale;
   long long* trace;                  // diagnostics: [blocks][layers][MEGA_TRACE_EV] wall clocks, or null
