@@ -492,19 +492,27 @@ extern "C" int mx_llm_finalize(mx_llm* x) {
 }
 
 // ---- one forward over `R` rows (decode rows or prefill rows) -------------------------
-// Multi-row attention: 32-position chunks per wave.  Longer splits avoid the cross-block merge
-// but shrink the grid; take the longest split (4, 2 chunks) that still gives >= 256 blocks
-// (one per CU), else 1.  At 32 rows and L ~600 this picks 4 (measured -14 % attention time vs
-// 1); at 8 rows it keeps 1 (4 would leave 64 blocks).
+// Multi-row attention: 32-position chunks per wave.  An 8-wave attention block needs ~250
+// VGPRs per wave, so it fills a CU: the grid should be ONE round of <= 256 blocks.  Give each
+// (row, kv head) pair 256 / pairs splits (at least 1) and every wave ceil(chunks / (splits *
+// waves)) chunks, rounded up to an instantiated count.  Measured (scripts/gpu_attn*.sh, 32 rows):
+// at L = 1200 the old "largest of {4, 2} with >= 256 blocks" rule made 512 blocks in two uneven
+// rounds (42.5 us); one split of <= 5 chunks per wave (the CPW 6 kernel) is one round
+// (27.2 us, 5.8 TB/s).  CPW 6 / 8 run a runtime chunk loop (a full unroll spills); at L = 2048
+// CPW 8 is 49.5 us against 53.0 us for two rounds of CPW 4.
+static int att_cpw_pick(int want, int nw) {
+  if (nw != 8) return want <= 1 ? 1 : want <= 2 ? 2 : 4;
+  if (want <= 4) return want < 1 ? 1 : want;
+  return want <= 6 ? 6 : 8;
+}
 static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
   if (R == 1) return x->att_cpw_b1;
   if (x->att_cpw_batch > 0) return x->att_cpw_batch;
-  for (int cpw : {4, 2}) {
-    const int S = 32 * x->att_nw_batch * cpw;
-    const long blocks = (long)((max_len + S - 1) / S) * x->c.kv_heads * R;
-    if (blocks >= 256) return cpw;
-  }
-  return 1;
+  const int nw = x->att_nw_batch;
+  const int pairs = R * x->c.kv_heads;
+  const int splits = std::max(1, 256 / pairs);
+  const int chunks = (max_len + 31) / 32;
+  return att_cpw_pick((chunks + splits * nw - 1) / (splits * nw), nw);
 }
 
 struct RowSet {
@@ -762,7 +770,7 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   // the persistent one-row step reads the length on the device: one graph for every length
   const bool mega = mega_eligible(x, n_rows, decode_max_len(x, n_rows));
   // (the chunk count is part of the key: one nsplit can come from two chunk counts)
-  const int key = mega ? -1 : (n_rows * 8 + cpw) * 4096 + nsplit;
+  const int key = mega ? -1 : (n_rows * 16 + cpw) * 4096 + nsplit;
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
@@ -993,8 +1001,10 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     }
     x->mega_ring = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
-    if (value != 1 && value != 2 && value != 4 && !(value == 0 && k == "att_cpw_batch"))
-      MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4 (att_cpw_batch also 0 = auto)");
+    const bool any = value == 1 || value == 2 || value == 4;
+    const bool wide = value == 3 || value == 6 || value == 8;  // 8-wave blocks only
+    if (!(any || (wide && k == "att_cpw_batch") || (value == 0 && k == "att_cpw_batch")))
+      MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4 (att_cpw_batch also 3/6/8, 0 = auto)");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
   } else {
     MX_FAIL(x, MX_ERR_ARG, "unknown option " + k);

@@ -516,11 +516,11 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
   f32x4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ch = 0; ch < CPW; ++ch) {
-    const int cb = ch & 1;
+  // one chunk; false once the wave runs past the context (wave-uniform).  cb (the K / V
+  // register buffer) must fold to a constant at every call site.
+  auto chunk = [&](const int ch, const int cb) __attribute__((always_inline)) -> bool {
     const int base = base0 + ch * 32 * NW;
-    if (base >= L) break;  // wave-uniform
+    if (base >= L) return false;
     if (ch + 1 < CPW && base + 32 * NW < L) load_kv(base + 32 * NW, cb ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     // scores
@@ -574,6 +574,22 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt)
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt], vb, acc[t], 0, 0, 0);
+    }
+    return true;
+  };
+  if constexpr (CPW <= 4) {
+#pragma unroll
+    for (int ch = 0; ch < CPW; ++ch)
+      if (!chunk(ch, ch & 1)) break;
+  } else {
+    // longer splits: a fully unrolled loop spills (CPW 6 / 8: 100 / 180 B scratch per lane);
+    // a runtime loop whose body is the CPW = 4 sequence: CPW 6 fits, CPW 8 spills 20 B
+#pragma unroll 1
+    for (int ch = 0; ch < CPW; ch += 4) {
+      if (!chunk(ch, 0)) break;
+      if (ch + 1 >= CPW || !chunk(ch + 1, 1)) break;
+      if (ch + 2 >= CPW || !chunk(ch + 2, 0)) break;
+      if (ch + 3 >= CPW || !chunk(ch + 3, 1)) break;
     }
   }
 
@@ -916,7 +932,8 @@ hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t s
     return hipGetLastError();                                                        \
   }
 #define MX_ATG(G_) MX_AT(G_, 1, 4) MX_AT(G_, 2, 4) MX_AT(G_, 4, 4) \
-                   MX_AT(G_, 1, 8) MX_AT(G_, 2, 8) MX_AT(G_, 4, 8)
+                   MX_AT(G_, 1, 8) MX_AT(G_, 2, 8) MX_AT(G_, 3, 8) MX_AT(G_, 4, 8) \
+                   MX_AT(G_, 6, 8) MX_AT(G_, 8, 8)
   MX_ATG(1) MX_ATG(2) MX_ATG(3) MX_ATG(4)
 #undef MX_ATG
 #undef MX_AT

@@ -176,13 +176,14 @@ def test_bad_args_fail_loudly():
         LlmEngine(cfg, bad, max_slots=1, max_pos=128)   # incomplete weights
 
 
-def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=None):
+def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=None,
+                  max_prefill=256):
     """Batched decode: every prompt on its own slot and decode row, all rows stepped together
     (the B >= 2 MFMA path); each row teacher-forced against its own oracle run."""
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
     eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=512, max_batch=max_batch or B,
-                    max_prefill=256)
+                    max_prefill=max_prefill)
     for k, v in (options or {}).items():
         eng.set_option(k, v)
     eng.enable_logits()
@@ -233,6 +234,20 @@ def test_batched_decode_40_rows_small():
     rng = np.random.default_rng(8)
     prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 3 + i)] for i in range(40)]
     assert _compare_rows(cfg, w, prompts, 6) >= 0.8 * 40 * 6
+
+
+@pytest.mark.parametrize("cpw", [0, 3, 6, 8])
+def test_batched_attention_chunk_counts_long_ragged(cpw):
+    """Multi-row attention with several 32-position chunks per wave: ragged contexts of
+    250..481 positions, 8 rows.  cpw 0 = the one-round auto choice (capi.hip att_cpw_auto);
+    3 / 6 / 8 force the 8-wave instantiations (one split up to 768 / 1536 / 2048 positions;
+    6 and 8 run the unroll-by-4 runtime chunk loop)."""
+    cfg = _cfgs("small")
+    w = synthetic_llm_weights(cfg, seed=41, std=0.05, norm_jitter=0.5)
+    rng = np.random.default_rng(42 + cpw)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 250 + 33 * i)] for i in range(8)]
+    assert _compare_rows(cfg, w, prompts, 4, options={"att_cpw_batch": cpw},
+                         max_prefill=512) >= 0.8 * 8 * 4
 
 
 def test_batched_decode_orpheus_width_4_rows():
