@@ -21,7 +21,7 @@ def main():
     cfg = C.OrpheusConfig(layers=1, vocab=1024)
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
     llm = LlmEngine(cfg, w, device=0, max_slots=32, max_pos=4096, max_batch=32, max_prefill=64)
-    llm.set_option("att_nw_batch", args.nw)
+    llm.set_option("att_nw_batch" if args.rows > 1 else "att_nw", args.nw)
     for L in [int(s) for s in args.lens.split(",")]:
         us = llm.bench_attention(L, args.rows, args.cpw, 0)
         kv = args.rows * L * cfg.kv_heads * 128 * 2 * 2
