@@ -61,12 +61,7 @@ def pmc_traffic(kind):
         return None
 
 
-def synthetic_audio_ids(n, seed):
-    import numpy as np
-    from project_morpheus_amd.config import AUDIO_CODE_BASE
-    rng = np.random.default_rng(seed)
-    codes = rng.integers(1, 4096, size=n)
-    return [int(AUDIO_CODE_BASE + 4096 * (i % 7) + c) for i, c in enumerate(codes)]
+from project_morpheus_amd.config import synthetic_audio_ids  # noqa: E402
 
 
 def cpu_baseline(cfg, prompt, n_decode=6):
@@ -419,10 +414,10 @@ def main():
     gu_gbs = gu_bytes / (gu_us * 1e-6) / 1e9
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(3):
-        llm.decode(1, 1.1, st)
+        llm.decode(1, st)
     prof = {}
     for _ in range(args.profile_steps):
-        for k, v in llm.decode_profiled(1, 1.1, st).items():
+        for k, v in llm.decode_profiled(1, st).items():
             prof[k] = prof.get(k, 0.0) + v
     per_step_us = {k: round(1e3 * v / args.profile_steps, 2) for k, v in prof.items()}
     llm.release_row(0, st)
@@ -432,10 +427,10 @@ def main():
     n_rep = 50
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(args.step_pos - len(prompt)):   # measure the step at a mid-utterance length
-        llm.decode(1, 1.1, st)
+        llm.decode(1, st)
     ev0.record(st)
     for _ in range(n_rep):
-        llm.decode(1, 1.1, st)
+        llm.decode(1, st)
     ev1.record(st)
     ev1.synchronize()
     step_ms = ev0.elapsed_time(ev1) / n_rep

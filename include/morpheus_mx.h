@@ -57,6 +57,17 @@ typedef struct mx_llm_config {
   int32_t wdtype;       /* MX_WEIGHTS_BF16 | MX_WEIGHTS_FP8 (BASELINE configs[4]) */
 } mx_llm_config;
 
+/* Per-stream generation parameters (engine_class.py:106-112 SamplingParams; inference.py:75-105).
+ * temperature <= 0 selects greedy decoding (argmax after the penalty; the parity mode).
+ * Otherwise: logits / temperature -> nucleus of mass top_p -> one draw from a Philox4x32-10
+ * stream keyed by `seed` and counted by position (definition in csrc/sample_kernels.hip). */
+typedef struct mx_sampling {
+  float temperature;
+  float top_p;
+  float repetition_penalty; /* HF/vLLM rule on the prompt + generated set (1.1 in Orpheus) */
+  uint64_t seed;
+} mx_sampling;
+
 /* ---- library / memory -------------------------------------------------------------- */
 const char* mx_version(void);
 int mx_host_alloc(size_t bytes, void** host_ptr, void** dev_ptr); /* pinned, device-mapped */
@@ -73,18 +84,19 @@ int mx_llm_set_weight(mx_llm* ctx, const char* name, const void* dev_data, int64
 /* RoPE tables [n_pos][head_dim/2] fp32 (host memory), llama3-scaled frequencies. */
 int mx_llm_set_rope(mx_llm* ctx, const float* cos_host, const float* sin_host, int n_pos);
 int mx_llm_finalize(mx_llm* ctx);
-/* Prefill prompt ids (host) into `slot`, bind the slot to decode row `row`, pick the first
- * token greedily under `penalty` (engine_class.py:106-112).  Enqueued on `stream`. */
+/* Prefill prompt ids (host) into `slot`, bind the slot to decode row `row`, set the slot's
+ * generation parameters, pick the first token.  Enqueued on `stream`. */
 int mx_llm_prefill(mx_llm* ctx, int slot, int row, const int32_t* ids_host, int n_ids,
-                   float penalty, void* stream);
-/* One greedy decode step for rows [0, n_rows) (hipGraph-captured per n_rows; replayed). */
-int mx_llm_decode(mx_llm* ctx, int n_rows, float penalty, void* stream);
+                   const mx_sampling* params, void* stream);
+/* One decode step for rows [0, n_rows), each under its slot's parameters (hipGraph-captured
+ * per row count and attention grid; replayed). */
+int mx_llm_decode(mx_llm* ctx, int n_rows, void* stream);
 /* Same step launched eagerly (no graph) with HIP events around every launch; adds the
  * elapsed milliseconds per launch class to ms_by_class[k] (k < n_classes; classes:
  * 0 qkv, 1 attention, 2 o-proj, 3 gate/up, 4 down, 5 lm_head+argmax, 6 commit).
  * Synchronises the stream.  Used by bench.py for the roofline of individual kernels. */
-int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, float penalty, void* stream,
-                           double* ms_by_class, int n_classes);
+int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_class,
+                           int n_classes);
 /* Tuning knobs ("legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "att_cpw",
  * "att_cpw_batch"; see capi.hip).  Drops the
  * captured graphs so the next mx_llm_decode re-captures with the new choice. */
@@ -103,17 +115,11 @@ int mx_llm_bench_attention(mx_llm* ctx, int L, int n_rows, int cpw, int debug, i
                            float* us_out);
 /* Park decode row `row` on the scratch slot (stream ended / barge-in reset). */
 int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
+/* Host view of decode row `row`: *active = 1 while a stream is bound to it (prefill until
+ * release), *next_pos = the position its next token takes. */
+int mx_llm_row_state(const mx_llm* ctx, int row, int* active, int* next_pos);
 /* Host-mapped token history [max_slots][max_pos] int32 written by the device. */
 int32_t* mx_llm_history(mx_llm* ctx);
-/* Persistent one-row decode step (one launch for all layers, Orpheus-3B shapes only):
- * *eligible = 1 when one-row mx_llm_decode graphs use it (option "mega", shape and
- * co-residency checks); *status = its last launch's give-up code (0 = every in-launch
- * hand-off completed).  Synchronises `stream`. */
-int mx_llm_mega_info(mx_llm* ctx, int* eligible, int* status, void* stream);
-/* Diagnostics (option "mega_trace" = 1): copy the per-block, per-layer event wall clocks
- * (100 MHz) of the last persistent step, [256 blocks][layers][16 events]; returns the count
- * copied or a negative error.  Synchronises the device. */
-int64_t mx_llm_mega_trace(mx_llm* ctx, int64_t* host_out, int64_t n);
 /* Parity/debug: keep a copy of the penalised logits of each decode row (enable before the
  * first mx_llm_decode; costs one extra write per vocab entry) and read one row back. */
 int mx_llm_debug_logits(mx_llm* ctx, int enable);
@@ -132,12 +138,14 @@ int mx_snac_set_weight(mx_snac* ctx, const char* name, const void* dev_data, int
 int mx_snac_finalize(mx_snac* ctx);
 /* Decode `batch` windows of n_frames frames each.  frames: [batch][7*n_frames] SNAC codes in
  * speechpipe token order (0..4095; the caller applies the range check of speechpipe.py:108-111).
- * noise: [batch][sum of the 4 NoiseBlock lengths] or NULL (fresh N(0,1) from `seed`).
+ * noise: [batch][sum of the 4 NoiseBlock lengths] or NULL: fresh N(0,1) drawn from `seeds[b]`
+ * per window (device-accessible [batch], e.g. host-mapped; a window's noise then depends on
+ * its own seed only) or, with seeds NULL, from `seed` over the whole batch.
  * pcm: [batch][hi-lo] int16 of samples [lo,hi) (NULL to skip); audio: [batch][2048*n_frames]
  * fp32 full window (NULL to skip). */
 int mx_snac_decode(mx_snac* ctx, const int32_t* frames, int n_frames, int batch,
-                   const float* noise, uint64_t seed, int16_t* pcm, float* audio, int lo,
-                   int hi, void* stream);
+                   const float* noise, uint64_t seed, const uint64_t* seeds, int16_t* pcm,
+                   float* audio, int lo, int hi, void* stream);
 const char* mx_snac_last_error(const mx_snac* ctx);
 void mx_snac_destroy(mx_snac* ctx);
 

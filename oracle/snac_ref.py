@@ -27,6 +27,8 @@ restatement is pinned only structurally (shapes, lengths, 2048 samples per frame
 from __future__ import annotations
 
 import math
+
+import numpy as np
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -94,4 +96,37 @@ def noise_lengths(n_frames: int) -> List[int]:
     for s in RATES:
         t *= s
         out.append(t)
+    return out
+
+
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = (z + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(_M64)
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(_M64)
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & np.uint64(_M64)
+    return z ^ (z >> np.uint64(31))
+
+
+def device_noise(seed: int, n: int) -> np.ndarray:
+    """Restatement of the GPU's NoiseBlock noise for a window seeded ``seed`` (csrc/
+    snac_kernels.hip gauss_kernel): element j = Box-Muller of mix64(seed ^ mix64(j)), float32.
+    Lets the end-to-end tests compare audio with the noise ON (host libm vs device ulps)."""
+    with np.errstate(over="ignore"):
+        j = np.arange(n, dtype=np.uint64)
+        h = _mix64(np.uint64(seed) ^ _mix64(j))
+    u1 = ((h >> np.uint64(40)).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777217.0)
+    u2 = ((h >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (np.sqrt(np.float32(-2.0) * np.log(u1)) *
+            np.cos(np.float32(6.283185307179586) * u2)).astype(np.float32)
+
+
+def window_noise(seed: int, n_frames: int) -> List[torch.Tensor]:
+    """The four NoiseBlock inputs [1,1,T_b] of one window drawn as the device draws them."""
+    z = device_noise(seed, sum(noise_lengths(n_frames)))
+    out, off = [], 0
+    for t in noise_lengths(n_frames):
+        out.append(torch.from_numpy(z[off:off + t].copy()).reshape(1, 1, t))
+        off += t
     return out

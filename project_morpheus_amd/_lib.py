@@ -38,6 +38,12 @@ class LlmConfig(C.Structure):
         ("eps", C.c_float), ("tied", C.c_int32), ("wdtype", C.c_int32)]
 
 
+class Sampling(C.Structure):
+    """mx_sampling: temperature <= 0 is greedy (the parity mode)."""
+    _fields_ = [("temperature", C.c_float), ("top_p", C.c_float),
+                ("repetition_penalty", C.c_float), ("seed", C.c_uint64)]
+
+
 _P = C.c_void_p
 _SIGS = {
     "mx_version": (C.c_char_p, []),
@@ -47,19 +53,17 @@ _SIGS = {
     "mx_llm_set_weight": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int]),
     "mx_llm_set_rope": (C.c_int, [_P, _P, _P, C.c_int]),
     "mx_llm_finalize": (C.c_int, [_P]),
-    "mx_llm_prefill": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int, C.c_float, _P]),
-    "mx_llm_decode": (C.c_int, [_P, C.c_int, C.c_float, _P]),
-    "mx_llm_decode_profiled": (C.c_int, [_P, C.c_int, C.c_float, _P,
-                                         C.POINTER(C.c_double), C.c_int]),
+    "mx_llm_prefill": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int, C.POINTER(Sampling), _P]),
+    "mx_llm_decode": (C.c_int, [_P, C.c_int, _P]),
+    "mx_llm_decode_profiled": (C.c_int, [_P, C.c_int, _P, C.POINTER(C.c_double), C.c_int]),
     "mx_llm_set_option": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "mx_llm_bench_gemv": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float),
                                     C.POINTER(C.c_double)]),
     "mx_llm_bench_attention": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.POINTER(C.c_float)]),
     "mx_llm_release_row": (C.c_int, [_P, C.c_int, _P]),
+    "mx_llm_row_state": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mx_llm_history": (C.POINTER(C.c_int32), [_P]),
-    "mx_llm_mega_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), _P]),
-    "mx_llm_mega_trace": (C.c_int64, [_P, C.POINTER(C.c_int64), C.c_int64]),
     "mx_llm_debug_logits": (C.c_int, [_P, C.c_int]),
     "mx_llm_read_logits": (C.c_int, [_P, C.c_int, _P, _P]),
     "mx_llm_last_error": (C.c_char_p, [_P]),
@@ -67,7 +71,7 @@ _SIGS = {
     "mx_snac_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
     "mx_snac_set_weight": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int]),
     "mx_snac_finalize": (C.c_int, [_P]),
-    "mx_snac_decode": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_uint64, _P, _P,
+    "mx_snac_decode": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_uint64, _P, _P, _P,
                                  C.c_int, C.c_int, _P]),
     "mx_snac_last_error": (C.c_char_p, [_P]),
     "mx_snac_destroy": (None, [_P]),

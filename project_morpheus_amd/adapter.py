@@ -11,9 +11,14 @@ Registered into Morpheus's registry as ``"mi355x"`` via ``register(registry)`` w
 ``mx_describe`` (keys of adapter_registry.py:51-60) and ``mx_voice_mapper``
 (adapter_registry.py:39-45 semantics).
 
-Synthesis runs in a producer thread (the engine loop must keep the GPU queue full while
-the orchestrator makes its small pulls); ``pull`` awaits the next chunk through
-``asyncio.to_thread`` like llama_local.py:79.
+Synthesis runs in a producer thread (the source is a blocking iterator; the engine loop
+must keep the GPU queue full while the orchestrator makes its small pulls).  ``pull`` first
+takes whatever the producer has already queued without leaving the event loop, and awaits
+the next chunk through ``asyncio.to_thread`` (like llama_local.py:79) only when the buffer
+cannot cover the request.  The producer never blocks indefinitely: it puts with a timeout
+and gives up once cancelled, and ``reset`` drains the old queue, so a barge-in or a client
+that stops pulling cannot wedge the service (the GPU stream is cancelled and its KV row
+freed through the source generator's ``finally``).
 """
 from __future__ import annotations
 
@@ -30,13 +35,27 @@ _END = object()
 
 def _default_source(prompt: str, voice: str, use_batching: bool, max_batch_chars: int,
                     cancel: threading.Event) -> Iterator[bytes]:
+    """Every long-form part is submitted at once (they decode as concurrent rows of the
+    GPU's batch) and their PCM is yielded in part order."""
     from .service import get_service
     svc = get_service()
-    for part in I.batch_sentences(prompt, max_batch_chars, use_batching):
-        for pcm in svc.stream(part, voice, cancel=cancel):
-            yield pcm
-        if cancel.is_set():
-            return
+    handles = [svc.submit(part, voice) for part in
+               I.batch_sentences(prompt, max_batch_chars, use_batching)]
+    try:
+        for h in handles:
+            while True:
+                if cancel.is_set():
+                    return
+                try:
+                    c = h.get(timeout=0.05)
+                except queue.Empty:
+                    continue
+                if c is None:
+                    break
+                yield c
+    finally:
+        for h in handles:
+            h.cancel()
 
 
 class MxTTSAdapter:
@@ -54,41 +73,59 @@ class MxTTSAdapter:
         self._q: Optional[queue.Queue] = None
         self._cancel: Optional[threading.Event] = None
         self._thread: Optional[threading.Thread] = None
-        self._error: Optional[BaseException] = None
 
     def _start(self) -> None:
         if self._q is not None or self._exhausted:
             return
         q: queue.Queue = queue.Queue(maxsize=64)
         cancel = threading.Event()
+        src = self.source(self.prompt, self.voice, self.use_batching, self.max_batch_chars,
+                          cancel)
+
+        def put(item) -> bool:
+            while not cancel.is_set():
+                try:
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    continue
+            return False
 
         def produce():
             try:
-                for pcm in self.source(self.prompt, self.voice, self.use_batching,
-                                       self.max_batch_chars, cancel):
-                    if cancel.is_set():
+                for pcm in src:
+                    if cancel.is_set() or not put(bytes(pcm)):
                         break
-                    q.put(bytes(pcm))
             except BaseException as e:  # surfaced to the caller of pull()
-                q.put(e)
+                put(e)
             finally:
-                q.put(_END)
+                close = getattr(src, "close", None)
+                if close is not None:
+                    close()  # runs the source's finally: GPU stream cancelled, row freed
+                put(_END)
 
         self._q, self._cancel = q, cancel
         self._thread = threading.Thread(target=produce, name="mx-tts", daemon=True)
         self._thread.start()
 
+    def _take(self, item) -> None:
+        if item is _END:
+            self._exhausted = True
+        elif isinstance(item, BaseException):
+            self._exhausted = True
+            raise item
+        else:
+            self._buffer.extend(item)
+
     async def pull(self, chunk_size: int) -> AudioChunk:
         self._start()
+        q = self._q
         while len(self._buffer) < chunk_size and not self._exhausted:
-            item = await asyncio.to_thread(self._q.get)
-            if item is _END:
-                self._exhausted = True
-                break
-            if isinstance(item, BaseException):
-                self._exhausted = True
-                raise item
-            self._buffer.extend(item)
+            try:
+                item = q.get_nowait()  # already produced: no thread hop
+            except queue.Empty:
+                item = await asyncio.to_thread(q.get)
+            self._take(item)
         if self._exhausted and not self._buffer:
             return AudioChunk(pcm=b"", duration_ms=0.0, eos=True)
         pcm = bytes(self._buffer[:chunk_size])
@@ -97,8 +134,16 @@ class MxTTSAdapter:
                           eos=self._exhausted and not self._buffer)
 
     async def reset(self) -> None:
+        """Barge-in (llama_local.py:152-157): cancel the utterance, drop buffered audio."""
         if self._cancel is not None:
             self._cancel.set()
+        q = self._q
+        if q is not None:  # unblock a producer waiting on a full queue
+            try:
+                while True:
+                    q.get_nowait()
+            except queue.Empty:
+                pass
         self._q = None
         self._cancel = None
         self._thread = None

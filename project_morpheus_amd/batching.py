@@ -1,4 +1,5 @@
-"""Continuous batching of concurrent utterance streams on one GPU (BASELINE configs 3 and 5).
+"""Continuous batching of concurrent utterance streams on one GPU (BASELINE configs 3-5, and
+the serving path behind every adapter).
 
 The reference serves concurrent requests by handing them to vLLM's continuous-batching
 engine, one request per thread (Orpheus-TTS/orpheus_tts_pypi/orpheus_tts/engine_class.py:
@@ -6,21 +7,34 @@ engine, one request per thread (Orpheus-TTS/orpheus_tts_pypi/orpheus_tts/engine_
 ``BatchSynthesizer`` is that loop for the MI355X engine:
 
 * every stream owns one KV slot and one decode row; a step decodes all rows at once
-  (``mx_llm_decode(n_rows)``, hipGraph per row count), rows without a stream are parked;
-* a new stream is admitted as soon as it has arrived and a row is free: its prefill is
-  enqueued between steps (ordered on the same HIP stream, nothing drains);
-* ``depth`` steps stay queued on the GPU; tokens are read from the host-mapped history
-  when a step's event completes, never by a per-token copy;
+  (``mx_llm_decode(n_rows)``, one hipGraph per row count), rows without a stream are parked
+  on the scratch slot; each row decodes under its own generation parameters (penalty,
+  temperature, top-p, seed: per-slot state set at prefill);
+* a stream is admitted as soon as it has arrived and a row is free: its prefill is enqueued
+  between steps (ordered on the same HIP stream, nothing drains);
+* ``depth`` steps stay queued on the GPU; tokens are read from the host-mapped history when
+  a step's event completes, never by a per-token copy;
+* a stream that has issued all its tokens is parked at once (its position never runs past
+  ``max_pos``); a cancelled stream (``StreamRequest.cancel``, the adapter's ``reset``) frees
+  its row at the next iteration and its undelivered audio is dropped;
 * each stream keeps the reference window schedule (``schedule.WindowScheduler``); the
   windows that become due in one host iteration are grouped by frame count and decoded by
   ONE batched SNAC call per group on a second HIP stream, PCM read from host-mapped memory.
+  NoiseBlock noise of window j of a stream is drawn from (stream noise seed, j) only, so a
+  stream's audio does not depend on what it was batched with.
+
+Two drivers share the loop: ``run(requests)`` (offline: arrival times, bench / long-form
+jobs) and ``start()`` + ``submit(request) -> StreamHandle`` (online: the per-GPU service the
+adapters use; a background thread owns the GPU).
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Deque, Dict, List, Optional, Sequence
+from typing import Callable, Deque, Dict, Iterator, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -30,20 +44,35 @@ from .config import STOP_IDS
 from .engine import SAMPLES_PER_FRAME, SLICE_HI, SLICE_LO, LlmEngine, SnacDecoder
 from .schedule import WindowScheduler, code_of_id
 
+_MASK48 = 0xFFFFFFFFFFFF
 
-@dataclass
+
+def window_seed(noise_seed: int, j: int) -> int:
+    """Noise seed of a stream's j-th SNAC window (batching-invariant)."""
+    return (noise_seed * 1000003 + j) & _MASK48
+
+
+@dataclass(eq=False)
 class StreamRequest:
     prompt_ids: Sequence[int]
     max_tokens: int
-    arrival: float = 0.0                    # seconds after run start
+    arrival: float = 0.0                    # seconds after run start (offline driver)
     inject_ids: Optional[Sequence[int]] = None  # synthetic audio ids (bench, random weights)
     stop_ids: Sequence[int] = STOP_IDS
     penalty: float = 1.1
+    temperature: float = 0.0                # <= 0: greedy (the parity mode)
+    top_p: float = 1.0
+    seed: int = 0                           # sampling stream (Philox key)
+    noise_seed: Optional[int] = None        # SNAC noise stream (None: assigned at admission)
+    on_chunk: Optional[Callable[["StreamRequest", bytes], None]] = None
+    on_done: Optional[Callable[["StreamRequest"], None]] = None
     # filled in by the synthesizer
     tokens: List[int] = field(default_factory=list)
-    pcm: List[bytes] = field(default_factory=list)
+    pcm: List[bytes] = field(default_factory=list)  # for callers that collect chunks here
     samples: int = 0
     windows: int = 0
+    cancelled: bool = False
+    error: Optional[BaseException] = None
     t_admit: Optional[float] = None
     t_first_audio: Optional[float] = None
     t_done: Optional[float] = None
@@ -58,6 +87,10 @@ class StreamRequest:
             return None
         return 1e3 * (self.t_first_audio - self.arrival)
 
+    def cancel(self) -> None:
+        """Barge-in: the loop frees the row at its next iteration, nothing more is emitted."""
+        self.cancelled = True
+
 
 class _Row:
     def __init__(self, idx: int):
@@ -66,24 +99,67 @@ class _Row:
         self.sched: Optional[WindowScheduler] = None
         self.n0 = 0          # prompt length (position of generated token 0)
         self.issued = 0      # generated tokens whose step has been enqueued
+        self.limit = 0       # tokens this row may issue (max_tokens clipped to max_pos)
+        self.parked = False  # released on the device (all tokens issued / stopped)
         self.stopped = False
 
 
 class _BatchRing:
-    """Host-mapped staging for batched SNAC calls: codes in, PCM16 out, zero-copy."""
+    """Host-mapped staging for batched SNAC calls: codes and noise seeds in, PCM16 out."""
 
     def __init__(self, n: int, max_batch: int, max_frames: int):
         self.n, self.max_batch = n, max_batch
         self.cbytes = max_batch * 7 * max_frames * 4
+        self.sbytes = max_batch * 8
         self.pbytes = max_batch * (SLICE_HI - SLICE_LO) * 2
-        self.buf = _lib.HostBuffer(n * (self.cbytes + self.pbytes))
-        self.codes = [self.buf.view(np.int32, max_batch * 7 * max_frames, i * self.cbytes)
+        per = (self.cbytes + self.sbytes + self.pbytes + 255) // 256 * 256
+        self.buf = _lib.HostBuffer(n * per)
+        self.codes = [self.buf.view(np.int32, max_batch * 7 * max_frames, i * per)
                       for i in range(n)]
-        base = n * self.cbytes
+        self.seeds = [self.buf.view(np.uint64, max_batch, i * per + self.cbytes)
+                      for i in range(n)]
         self.pcm = [self.buf.view(np.int16, max_batch * (SLICE_HI - SLICE_LO),
-                                  base + i * self.pbytes) for i in range(n)]
-        self.codes_dev = [self.buf.dev_ptr(i * self.cbytes) for i in range(n)]
-        self.pcm_dev = [self.buf.dev_ptr(base + i * self.pbytes) for i in range(n)]
+                                  i * per + self.cbytes + self.sbytes) for i in range(n)]
+        self.codes_dev = [self.buf.dev_ptr(i * per) for i in range(n)]
+        self.seeds_dev = [self.buf.dev_ptr(i * per + self.cbytes) for i in range(n)]
+        self.pcm_dev = [self.buf.dev_ptr(i * per + self.cbytes + self.sbytes) for i in range(n)]
+
+
+class StreamHandle:
+    """Online stream: PCM chunks arrive through a queue filled by the loop thread (never
+    blocks the loop: the queue is unbounded, one utterance is at most ~1 MB of PCM)."""
+
+    _END = object()
+
+    def __init__(self, req: StreamRequest):
+        self.req = req
+        self._q: "queue.Queue" = queue.Queue()
+
+    def _chunk(self, req, data: bytes) -> None:
+        self._q.put(data)
+
+    def _done(self, req) -> None:
+        self._q.put(self._END)
+
+    def get(self, timeout: Optional[float] = None):
+        """Next PCM chunk, or None at the end of the stream; re-raises a loop failure."""
+        item = self._q.get(timeout=timeout)
+        if item is self._END:
+            self._q.put(self._END)  # the end stays visible to later calls
+            if self.req.error is not None:
+                raise self.req.error
+            return None
+        return item
+
+    def chunks(self) -> Iterator[bytes]:
+        while True:
+            c = self.get()
+            if c is None:
+                return
+            yield c
+
+    def cancel(self) -> None:
+        self.req.cancel()
 
 
 class BatchSynthesizer:
@@ -95,64 +171,187 @@ class BatchSynthesizer:
         self.snac_stream = torch.cuda.Stream(llm.device)
         self.ring = _BatchRing(16, snac.max_batch, snac.max_frames)
         self._calls = 0
+        self._admitted = 0
+        self._live: List[StreamRequest] = []
+        # online driver
+        self._inbox: Deque[StreamRequest] = deque()
+        self._cv = threading.Condition()
+        self._thread: Optional[threading.Thread] = None
+        self._stop = False
+        self._t0 = time.perf_counter()
+        self.outstanding_tokens = 0  # tokens still owed to submitted streams (dispatch load)
 
     # ---------------------------------------------------------------------------------
     def run(self, requests: List[StreamRequest], on_chunk=None) -> float:
         """Serve ``requests`` (admitted in arrival order) to completion; returns wall seconds.
         ``on_chunk(request, pcm_bytes)`` is called for every non-empty PCM chunk in order."""
+        waiting: Deque[StreamRequest] = deque(sorted(requests, key=lambda r: r.arrival))
+        if on_chunk is not None:
+            for r in waiting:
+                r.on_chunk = r.on_chunk or on_chunk
+        n = len(waiting)
+        finished = [0]
+
+        def done_cb(_req):
+            finished[0] += 1
+
+        t0 = time.perf_counter()
+
+        def poll(now):
+            out = []
+            while waiting and waiting[0].arrival <= now:
+                out.append(waiting.popleft())
+            return out
+
+        def idle(now):
+            if waiting:
+                time.sleep(max(0.0, min(0.001, waiting[0].arrival - now)))
+
+        self._loop(t0, poll, idle, lambda: finished[0] >= n and not waiting, done_cb)
+        return time.perf_counter() - t0
+
+    # ---------------------------------------------------------------------------------
+    def start(self) -> "BatchSynthesizer":
+        """Online mode: a daemon thread owns the GPU and serves ``submit``-ted streams."""
+        if self._thread is None:
+            self._t0 = time.perf_counter()
+            self._stop = False
+            self._thread = threading.Thread(target=self._serve, name="mx-batch", daemon=True)
+            self._thread.start()
+        return self
+
+    def submit(self, req: StreamRequest) -> StreamHandle:
+        if self._thread is None:
+            self.start()
+        h = StreamHandle(req)
+        req.on_chunk, req.on_done = h._chunk, h._done
+        req.arrival = time.perf_counter() - self._t0
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("BatchSynthesizer stopped")
+            self._inbox.append(req)
+            self.outstanding_tokens += req.max_tokens
+            self._cv.notify()
+        return h
+
+    def stop(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def _serve(self) -> None:
+        def poll(now):
+            with self._cv:
+                out = list(self._inbox)
+                self._inbox.clear()
+            return out
+
+        def idle(now):
+            with self._cv:
+                if not self._inbox and not self._stop:
+                    self._cv.wait(timeout=0.05)
+
+        def done_cb(req):
+            with self._cv:
+                self.outstanding_tokens -= req.max_tokens
+
+        try:
+            self._loop(self._t0, poll, idle, lambda: self._stop, done_cb)
+        except BaseException as e:  # fail every stream loudly, never hang a consumer
+            with self._cv:
+                self._stop = True
+                orphans = list(self._inbox) + list(self._live)
+                self._inbox.clear()
+            for req in orphans:
+                req.error = e
+                if req.on_done is not None:
+                    req.on_done(req)
+            raise
+
+    # ---------------------------------------------------------------------------------
+    def _loop(self, t0: float, poll, idle, finished, done_cb) -> None:
         llm, B = self.llm, self.llm.max_batch
         rows = [_Row(i) for i in range(B)]
-        waiting: Deque[StreamRequest] = deque(sorted(requests, key=lambda r: r.arrival))
+        waiting: Deque[StreamRequest] = deque()
         inflight: Deque = deque()   # (event, [(row, req, k)])
         pending: Deque = deque()    # (event, ring index, [(req, nbytes)])
-        t0 = time.perf_counter()
-        done = 0
+        closing: Deque = deque()    # streams whose end waits for their last SNAC call
+        live = self._live
 
         def now():
             return time.perf_counter() - t0
 
-        def active_rows():
-            return [r for r in rows if r.req is not None and not r.stopped]
+        def complete(req: StreamRequest) -> None:
+            req.t_done = now()
+            if any(q is req for q in live):
+                live.remove(req)
+            done_cb(req)
+            if req.on_done is not None:
+                req.on_done(req)
+
+        def park(r: _Row):
+            if not r.parked:
+                llm.release_row(r.idx, self.stream)
+                r.parked = True
 
         def admit():
             for r in rows:
-                if not waiting or waiting[0].arrival > now():
+                if not waiting:
                     return
-                if r.req is None:
-                    req = waiting.popleft()
-                    r.req, r.sched, r.n0 = req, WindowScheduler(), len(req.prompt_ids)
-                    r.issued, r.stopped = 1, False
-                    req.t_admit = now()
-                    llm.prefill(r.idx, r.idx, req.prompt_ids, req.penalty, self.stream)
-                    ev = torch.cuda.Event()
-                    ev.record(self.stream)
-                    inflight.append((ev, [(r, req, 0)]))
+                if r.req is not None:
+                    continue
+                req = waiting.popleft()
+                if req.cancelled:
+                    complete(req)
+                    continue
+                n0 = len(req.prompt_ids)
+                if n0 < 1 or n0 > llm.max_prefill or n0 >= llm.max_pos:
+                    req.error = ValueError(f"prompt of {n0} ids does not fit (max_prefill "
+                                           f"{llm.max_prefill}, max_pos {llm.max_pos})")
+                    complete(req)
+                    continue
+                if req.noise_seed is None:
+                    req.noise_seed = (self.seed * 1000003 + self._admitted) & _MASK48
+                self._admitted += 1
+                r.req, r.sched, r.n0 = req, WindowScheduler(), n0
+                r.limit = max(1, min(req.max_tokens, llm.max_pos - n0))
+                r.issued, r.stopped, r.parked = 1, False, False
+                req.t_admit = now()
+                live.append(req)
+                llm.prefill(r.idx, r.idx, req.prompt_ids, req.penalty, self.stream,
+                            temperature=req.temperature, top_p=req.top_p, seed=req.seed)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                inflight.append((ev, [(r, req, 0)]))
+                if r.issued >= r.limit:
+                    park(r)
 
         def launch_windows(due: List):
-            """due: [(req, window codes)] -> one SNAC call per frame-count group."""
+            """due: [(req, window index, codes)] -> one SNAC call per frame-count group."""
             groups: Dict[int, List] = {}
-            for req, win in due:
-                groups.setdefault(len(win) // 7, []).append((req, win))
+            for item in due:
+                groups.setdefault(len(item[2]) // 7, []).append(item)
             for nf, items in groups.items():
                 for s in range(0, len(items), self.ring.max_batch):
                     chunk = items[s:s + self.ring.max_batch]
                     i = self._calls % self.ring.n
                     while len(pending) >= self.ring.n:
                         drain(block=True, upto=1)
-                    codes = self.ring.codes[i]
-                    for j, (_, win) in enumerate(chunk):
+                    codes, seeds = self.ring.codes[i], self.ring.seeds[i]
+                    for j, (req, widx, win) in enumerate(chunk):
                         codes[j * 7 * nf:(j + 1) * 7 * nf] = win[:7 * nf]
+                        seeds[j] = window_seed(req.noise_seed, widx)
                     lo, hi = SLICE_LO, min(SLICE_HI, SAMPLES_PER_FRAME * nf)
                     hi = max(lo, hi)
-                    self.snac.decode_ptr(self.ring.codes_dev[i], nf, len(chunk), 0,
-                                         (self.seed * 1000003 + self._calls) & 0xFFFFFFFFFFFF,
+                    self.snac.decode_ptr(self.ring.codes_dev[i], nf, len(chunk), 0, 0,
                                          self.ring.pcm_dev[i] if hi > lo else 0, 0, lo, hi,
-                                         self.snac_stream)
+                                         self.snac_stream, seeds_ptr=self.ring.seeds_dev[i])
                     e = torch.cuda.Event()
                     e.record(self.snac_stream)
-                    pending.append((e, i, [(req, (hi - lo) * 2) for req, _ in chunk]))
-                    for req, _ in chunk:
-                        req.windows += 1
+                    pending.append((e, i, [(req, (hi - lo) * 2) for req, _, _ in chunk]))
                     self._calls += 1
 
         def drain(block: bool, upto: Optional[int] = None):
@@ -166,67 +365,86 @@ class BatchSynthesizer:
                 k += 1
                 pcm = self.ring.pcm[i]
                 for j, (req, nbytes) in enumerate(items):
-                    if not nbytes:
+                    if not nbytes or req.cancelled:
                         continue
                     n = nbytes // 2
                     data = pcm[j * n:(j + 1) * n].tobytes()
                     req.samples += n
                     if req.t_first_audio is None:
                         req.t_first_audio = now()
-                    if on_chunk is not None:
-                        on_chunk(req, data)
+                    if req.on_chunk is not None:
+                        req.on_chunk(req, data)
 
         def finish(r: _Row, due: List):
-            for win in r.sched.flush():
-                due.append((r.req, win))
-            r.req.t_done = now()
-            llm.release_row(r.idx, self.stream)
-            r.req, r.sched, r.stopped = None, None, False
+            req = r.req
+            if not req.cancelled:
+                for win in r.sched.flush():
+                    due.append((req, req.windows, win))
+                    req.windows += 1
+            park(r)
+            closing.append(req)
+            r.req, r.sched, r.stopped, r.parked = None, None, False, False
 
-        while done < len(requests):
+        def announce():
+            # a closing stream's windows were all launched when it closed: once no pending
+            # SNAC call holds one of them, its end is announced (in close order)
+            while closing:
+                req = closing[0]
+                if any(q is req for _, _, items in pending for q, _ in items):
+                    return
+                closing.popleft()
+                complete(req)
+
+        while True:
+            waiting.extend(poll(now()))
+            for r in rows:  # barge-in: free cancelled rows now
+                if r.req is not None and r.req.cancelled:
+                    finish(r, [])
             admit()
-            act = active_rows()
+            act = [r for r in rows if r.req is not None and not r.stopped and not r.parked]
             # keep `depth` steps queued for the rows that still need tokens
             while act and len(inflight) < self.depth:
                 n_rows = max(r.idx for r in act) + 1
-                need = [r for r in act if r.issued < r.req.max_tokens]
-                if not need:
-                    break
-                llm.decode(n_rows, need[0].req.penalty, self.stream)
+                llm.decode(n_rows, self.stream)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 entries = []
                 for r in act:
-                    if r.issued < r.req.max_tokens:
-                        entries.append((r, r.req, r.issued))
-                        r.issued += 1
+                    entries.append((r, r.req, r.issued))
+                    r.issued += 1
+                    if r.issued >= r.limit:
+                        park(r)
                 inflight.append((ev, entries))
+                act = [r for r in act if not r.parked]
             if not inflight:
-                if waiting:  # idle until the next arrival
-                    time.sleep(max(0.0, min(0.001, waiting[0].arrival - now())))
-                    continue
-                break
+                drain(block=bool(pending) and not waiting)
+                announce()
+                if finished() and not pending and not closing and not waiting and \
+                        all(r.req is None for r in rows):
+                    break
+                if not pending and not closing:
+                    idle(now())
+                continue
             ev, entries = inflight.popleft()
             ev.synchronize()
             due: List = []
             for r, req, k in entries:
-                if r.req is not req or r.stopped:
+                if r.req is not req or r.stopped or req.cancelled:
                     continue  # speculative step of a stream that already ended
                 tok = int(llm.hist[r.idx, r.n0 + k])
                 req.tokens.append(tok)
                 feed = int(req.inject_ids[k]) if req.inject_ids is not None else tok
                 for win in r.sched.push(code_of_id(feed, r.sched.count)):
-                    due.append((req, win))
-                if tok in req.stop_ids or len(req.tokens) >= req.max_tokens:
+                    due.append((req, req.windows, win))
+                    req.windows += 1
+                if tok in req.stop_ids or len(req.tokens) >= r.limit:
                     r.stopped = True
             for r in rows:
                 if r.req is not None and r.stopped:
                     finish(r, due)
-                    done += 1
             if due:
                 launch_windows(due)
             drain(block=False)
+            announce()
         for e, _ in inflight:
             e.synchronize()
-        drain(block=True)
-        return time.perf_counter() - t0

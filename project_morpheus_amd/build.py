@@ -11,8 +11,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmorpheus_mx.so")
-SOURCES = ["capi.hip", "llm_kernels.hip", "llm_batched.hip", "llm_batched_v4.hip", "llm_mega.hip",
-           "llm_batched_v7.hip", "snac_kernels.hip"]
+OBJ_DIR = os.path.join(CSRC, "build")  # per-translation-unit objects (git-ignored)
+SOURCES = ["capi.hip", "llm_kernels.hip", "llm_batched_v4.hip", "sample_kernels.hip",
+           "snac_kernels.hip"]
 HEADERS = ["mx_common.h", "mx_llm_kernels.h", "mx_snac_kernels.h"]
 ARCH = os.environ.get("MORPHEUS_MX_ARCH", "gfx950")
 
@@ -24,37 +25,56 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def _obj(s: str) -> str:
+    return os.path.join(OBJ_DIR, s.replace(".hip", ".o"))
+
+
+def _deps_mtime() -> float:
+    deps = [os.path.join(CSRC, h) for h in HEADERS]
+    deps.append(os.path.join(HERE, "..", "include", "morpheus_mx.h"))
+    return max(os.path.getmtime(d) for d in deps if os.path.exists(d))
+
+
+def _stale(s: str, hdr: float) -> bool:
+    o = _obj(s)
+    return not os.path.exists(o) or os.path.getmtime(o) < max(
+        hdr, os.path.getmtime(os.path.join(CSRC, s)))
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
+    hdr = _deps_mtime()
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(HERE, "..", "include", "morpheus_mx.h"))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return any(_stale(s, hdr) or os.path.getmtime(_obj(s)) > t for s in SOURCES)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the translation units that changed (all of them with ``force``), in parallel,
+    into csrc/build/, then link the shared library."""
     if not force and not needs_build():
         return LIB
-    objs, procs = [], []
-    for s in SOURCES:  # translation units compile in parallel
-        src = os.path.join(CSRC, s)
-        obj = os.path.join(CSRC, s.replace(".hip", ".o"))
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hdr = _deps_mtime()
+    procs = []
+    for s in SOURCES:
+        if not force and not _stale(s, hdr):
+            continue
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-               "-munsafe-fp-atomics", "-Wno-unused-result", "-x", "hip", "-c", src, "-o", obj]
+               "-munsafe-fp-atomics", "-Wno-unused-result", "-x", "hip", "-c",
+               os.path.join(CSRC, s), "-o", _obj(s) + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        procs.append((subprocess.Popen(cmd), cmd))
-        objs.append(obj)
-    for p, cmd in procs:
+        procs.append((subprocess.Popen(cmd), cmd, s))
+    for p, cmd, s in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
+        os.replace(_obj(s) + ".tmp", _obj(s))
     tmp = LIB + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + \
+        [_obj(s) for s in SOURCES]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
     return LIB
 
 

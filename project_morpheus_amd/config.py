@@ -113,3 +113,12 @@ MX_TOKENIZER = os.environ.get("MORPHEUS_MX_TOKENIZER")  # dir with tokenizer.jso
 MX_DEVICE = env_int("MORPHEUS_MX_DEVICE", 0)
 MX_MAX_POS = env_int("MORPHEUS_MX_MAX_POS", env_int("LLAMA_N_CTX", 8192))
 MX_MAX_SLOTS = env_int("MORPHEUS_MX_MAX_SLOTS", 8)
+MX_GPUS = env_int("MORPHEUS_MX_GPUS", 1)                # worker processes (one per GPU)
+
+
+def synthetic_audio_ids(n: int, seed: int):
+    """Seeded audio-token stream for synthetic weights: random weights never
+    speak, so the SNAC schedule consumes uniform codes in [1, 4095] per phase instead."""
+    rng = np.random.default_rng(seed)
+    codes = rng.integers(1, 4096, size=n)
+    return [int(AUDIO_CODE_BASE + 4096 * (i % 7) + c) for i, c in enumerate(codes)]

@@ -101,8 +101,11 @@ struct mx_llm {
   int32_t *pre_slot = nullptr, *pre_pos = nullptr, *pre_ids = nullptr;
   unsigned long long* best = nullptr;
   uint8_t* seen = nullptr;
-  float* penalty = nullptr;
-  float penalty_host = -1.f;
+  // per KV slot sampling state (set at prefill; the scratch slot stays greedy)
+  float *penalty = nullptr, *samp_temp = nullptr, *samp_top_p = nullptr;
+  uint32_t* samp_seed = nullptr;
+  float* logits = nullptr;      // [max_rows_head][vocab] penalised logits (sampling / parity)
+  int logits_all = 0;           // option via mx_llm_debug_logits: keep every row's logits
   int32_t* hist_host = nullptr;
   int32_t* hist_dev = nullptr;
   hipStream_t cap = nullptr;
@@ -112,7 +115,6 @@ struct mx_llm {
   std::map<int, hipGraph_t> graph_defs;
   bool final = false;
   int max_rows = 0;
-  float* logits_dbg = nullptr;  // [max_batch][vocab] when enabled
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
   int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
@@ -120,24 +122,12 @@ struct mx_llm {
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
-  int rows_kernel = 4;               // option: multi-row GEMM generation (4 measured fastest; 7, 5)
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
-  // persistent single-stream step (llm_mega.hip): eligible shapes + co-residency checked at
-  // create; option "mega" (default 0) picks it for one-row decode graphs
-  bool mega_ok = false;
-  int mega = 0, mega_ring = 32;  // measured slower than the per-kernel step
-  float *mega_ws = nullptr, *mega_part = nullptr, *h_fin = nullptr;
-  int* mega_sync = nullptr;
-  size_t mega_sync_bytes = 0;
-  void* mega_dummy = nullptr;
-  int mega_nsplit_cap = 0;
-  long long* mega_trace = nullptr;  // option "mega_trace": per-block event clocks of the last step
-  // every layer's matrices / norms / fp8 scales of one kind are contiguous (the persistent
-  // kernel walks layers by a fixed stride)
+  // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
   float *attn_norm_all = nullptr, *mlp_norm_all = nullptr;
@@ -253,9 +243,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
     for (auto& sh : shapes)
       for (int r : {16, 32, 64, sh[2]}) {
         size_t wf = 0, tk = 0;
-        gemm_rows_workspace(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
-        x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
-        x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
         v4::gemm_rows_workspace_v4(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
         x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
         x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
@@ -271,20 +258,11 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->pre_ids, c.max_prefill);
   A(x->best, c.max_batch);
   A(x->seen, (size_t)slots * c.vocab);
-  A(x->penalty, 1);
-  x->mega_ok = c.hidden == 3072 && c.heads == 24 && c.kv_heads == 8 && c.head_dim == 128 &&
-               c.ffn == 8192;
-  if (x->mega_ok) {
-    x->mega_nsplit_cap = std::min(c.max_pos / MEGA_SPLIT, MEGA_MAX_SPLITS);
-    x->mega_sync_bytes = (mega_sync_ints(c.layers) + mega_flag_ints(c.layers)) * 4;
-    A(x->mega_ws, NL * MEGA_WS_LAYER);
-    A(x->mega_part, NL * 8 * x->mega_nsplit_cap * MEGA_PART);
-    A(x->mega_sync, x->mega_sync_bytes / 4);
-    A(x->h_fin, c.hidden);
-    uint8_t* dm = nullptr;
-    A(dm, 128 * 1024);
-    x->mega_dummy = dm;
-  }
+  A(x->penalty, slots);
+  A(x->samp_temp, slots);
+  A(x->samp_top_p, slots);
+  A(x->samp_seed, 2 * slots);
+  A(x->logits, (size_t)c.max_batch * c.vocab);
 #undef A
   if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
@@ -310,6 +288,13 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess) e = hipMemset(x->rows_tickets, 0, x->rows_tickets_n * 4);
   if (e == hipSuccess) e = hipMemset(x->seen, 0, (size_t)slots * c.vocab);
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
+  if (e == hipSuccess) e = hipMemset(x->samp_temp, 0, slots * 4);  // greedy everywhere
+  if (e == hipSuccess) e = hipMemset(x->samp_seed, 0, slots * 8);
+  if (e == hipSuccess) {
+    std::vector<float> ones(slots, 1.0f);
+    e = hipMemcpy(x->penalty, ones.data(), slots * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(x->samp_top_p, ones.data(), slots * 4, hipMemcpyHostToDevice);
+  }
   // every decode row starts parked on the scratch slot at position 0
   std::vector<int32_t> park(c.max_batch, c.max_slots), zero(c.max_batch, 0);
   if (e == hipSuccess)
@@ -318,13 +303,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
     e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
   if (e == hipSuccess) e = gemv_prepare(std::max(std::max(c.hidden, c.ffn), c.heads * 128));
-  if (e == hipSuccess && x->mega_ok) {
-    e = hipMemset(x->mega_dummy, 0, 128 * 1024);
-    if (e == hipSuccess) e = hipMemset(x->mega_sync, 0, x->mega_sync_bytes);
-    int ok = 0;
-    if (e == hipSuccess) e = mega_resident(device, f8 ? 1 : 0, x->mega_ring, &ok);
-    x->mega_ok = ok != 0;
-  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
     g_err = std::string("init failed: ") + hipGetErrorString(e);
@@ -526,7 +504,6 @@ struct RowSet {
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_dbg = x->rows_dbg;
-  g.rows_kernel = x->rows_kernel;
   g.rows_pw = x->rows_pw;
   g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
@@ -619,16 +596,26 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
   return e;
 }
 
-static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot, int R,
-                               unsigned long long* best, hipStream_t st) {
+// lm_head + penalty + argmax for R rows, then the sampler for the rows whose slot samples
+// (greedy rows return at once).  `best` points into x->best; its offset selects the rows of
+// x->logits used.
+static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot,
+                               const int32_t* pos, int R, unsigned long long* best,
+                               hipStream_t st) {
   const auto& c = x->c;
+  float* lg = x->logits + (size_t)(best - x->best) * c.vocab;
   GemvArgs g{};
   attach_ws(x, g);
   g.R = R; g.eps = c.eps; g.W = x->lm; g.wscale = x->slm; g.wdtype = c.wdtype; g.N = c.vocab; g.K = c.hidden; g.X = h;
   g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
-  g.penalty = x->penalty; g.best = best;
-  g.logits = x->logits_dbg ? x->logits_dbg + (size_t)(best - x->best) * c.vocab : nullptr;
-  return launch_gemv(g, EPI_ARGMAX, true, st);
+  g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = best;
+  g.logits = lg; g.logits_all = x->logits_all;
+  hipError_t e = launch_gemv(g, EPI_ARGMAX, true, st);
+  if (e != hipSuccess) return e;
+  SampleArgs sa{};
+  sa.logits = lg; sa.row_slot = slot; sa.row_pos = pos; sa.temp = x->samp_temp;
+  sa.top_p = x->samp_top_p; sa.seed = x->samp_seed; sa.best = best; sa.V = c.vocab;
+  return launch_sample(sa, R, st);
 }
 
 // Longest attention span of the next step over rows [0, n_rows) (host mirror of row_pos).
@@ -645,7 +632,7 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hi
   RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw};
   hipError_t e = enqueue_layers(x, rs, st, prof);
   PROF_BEGIN(PK_HEAD);
-  if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, n_rows, x->best, st);
+  if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, x->row_pos, n_rows, x->best, st);
   PROF_END();
   PROF_BEGIN(PK_COMMIT);
   if (e == hipSuccess) {
@@ -660,54 +647,11 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hi
   return e;
 }
 
-// One-row step through the persistent kernel: memset of the hand-off words (a graph node),
-// the layers in one launch, then the lm_head / argmax and the commit as usual.
-static bool mega_eligible(const mx_llm* x, int n_rows, int max_len) {
-  return x->mega && x->mega_ok && n_rows == 1 && max_len <= x->mega_nsplit_cap * MEGA_SPLIT;
-}
-
-static hipError_t enqueue_decode_mega(mx_llm* x, hipStream_t st) {
-  const auto& c = x->c;
-  const bool f8 = c.wdtype == WT_FP8;
-  MegaArgs m{};
-  m.wqkv = x->wqkv_all; m.wo = x->wo_all; m.wgu = x->wgu_all; m.wd = x->wd_all;
-  m.sqkv = x->sqkv_all; m.so = x->so_all; m.sgu = x->sgu_all; m.sd = x->sd_all;
-  m.attn_norm = x->attn_norm_all; m.mlp_norm = x->mlp_norm_all;
-  m.rope_cos = x->rope_cos; m.rope_sin = x->rope_sin;
-  m.row_slot = x->row_slot; m.row_pos = x->row_pos;
-  m.kcache = x->kcache; m.vcache = x->vcache; m.kv_layer_elems = x->kv_layer_elems;
-  m.max_pos = c.max_pos; m.layers = c.layers; m.nsplit_cap = x->mega_nsplit_cap;
-  m.f8 = f8 ? 1 : 0; m.ring = x->mega_ring;
-  m.h_in = x->h_dec; m.h_out = x->h_fin; m.ws = x->mega_ws; m.part = x->mega_part;
-  m.sync = x->mega_sync; m.dummy = x->mega_dummy;
-  m.flags = x->mega_sync + mega_sync_ints(c.layers);
-  m.eps = c.eps; m.att_scale = 1.0f / sqrtf(128.0f);
-  m.trace = x->mega_trace;
-  hipError_t e = hipMemsetAsync(x->mega_sync, 0, x->mega_sync_bytes, st);
-  if (e == hipSuccess) e = launch_mega(m, st);
-  if (e == hipSuccess) e = enqueue_head(x, x->h_fin, x->row_slot, 1, x->best, st);
-  if (e == hipSuccess) {
-    CommitArgs cm{};
-    cm.best = x->best; cm.row_slot = x->row_slot; cm.row_pos = x->row_pos;
-    cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
-    cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
-    cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
-    e = launch_commit(cm, 1, st);
-  }
-  return e;
-}
-
-static int set_penalty(mx_llm* x, float p, hipStream_t st) {
-  if (p != x->penalty_host) {
-    MX_TRY(x, launch_set_scalar(x->penalty, p, st));
-    x->penalty_host = p;
-  }
-  return MX_OK;
-}
-
 extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, int n,
-                              float penalty, void* stream) {
-  if (!x || !ids) return MX_ERR_ARG;
+                              const mx_sampling* sp, void* stream) {
+  if (!x || !ids || !sp) return MX_ERR_ARG;
+  if (!(sp->repetition_penalty > 0.f) || !(sp->top_p > 0.f) || sp->temperature < 0.f)
+    MX_FAIL(x, MX_ERR_ARG, "sampling: need repetition_penalty > 0, top_p > 0, temperature >= 0");
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
   if (slot < 0 || slot >= c.max_slots || row < 0 || row >= c.max_batch)
@@ -717,7 +661,9 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
     if (ids[i] < 0 || ids[i] >= c.vocab) MX_FAIL(x, MX_ERR_ARG, "prompt id out of vocab");
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
+  MX_TRY(x, launch_set_slot_params(x->penalty, x->samp_temp, x->samp_top_p, x->samp_seed, slot,
+                                   sp->repetition_penalty, sp->temperature,
+                                   sp->top_p < 1.f ? sp->top_p : 1.f, sp->seed, st));
   MX_TRY(x, hipMemsetAsync(x->seen + (size_t)slot * c.vocab, 0, c.vocab, st));
   MX_TRY(x, hipMemcpyAsync(x->pre_ids, ids, (size_t)n * 4, hipMemcpyHostToDevice, st));
   MX_TRY(x, launch_set_rows(x->pre_slot, x->pre_pos, n, slot, 0, st));
@@ -726,8 +672,8 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n, att_cpw_auto(x, n, n)};
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
-  MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1), 1,
-                         x->best + row, st));
+  MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1),
+                         x->pre_pos + (n - 1), 1, x->best + row, st));
   // bind decode row -> slot at position n-1, then commit (advances to n)
   MX_TRY(x, launch_set_rows(x->row_slot + row, x->row_pos + row, 1, slot, n - 1, st));
   CommitArgs cm{};
@@ -754,29 +700,25 @@ static int check_room(mx_llm* x, int n_rows) {
   return MX_OK;
 }
 
-extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream) {
+extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (!x) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
   const int cpw = att_cpw_auto(x, n_rows, decode_max_len(x, n_rows));
   const int S = 32 * cpw * (n_rows == 1 ? x->att_nw_b1 : x->att_nw_batch);
   const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
-  // the persistent one-row step reads the length on the device: one graph for every length
-  const bool mega = mega_eligible(x, n_rows, decode_max_len(x, n_rows));
   // (the chunk count is part of the key: one nsplit can come from two chunk counts)
-  const int key = mega ? -1 : (n_rows * 16 + cpw) * 4096 + nsplit;
+  const int key = (n_rows * 16 + cpw) * 4096 + nsplit;
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
     MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
-    hipError_t e = mega ? enqueue_decode_mega(x, x->cap)
-                        : enqueue_decode(x, n_rows, nsplit * S, cpw, x->cap, nullptr);
+    hipError_t e = enqueue_decode(x, n_rows, nsplit * S, cpw, x->cap, nullptr);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(x->cap, &g);
     MX_TRY(x, e);
@@ -791,14 +733,13 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, float penalty, void* stream)
   return MX_OK;
 }
 
-extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, float penalty, void* stream,
+extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, void* stream,
                                       double* ms_by_class, int n_classes) {
   if (!x || !ms_by_class) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   if (n_rows < 1 || n_rows > x->c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (set_penalty(x, penalty, st)) return MX_ERR_HIP;
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   Prof prof;
   const int ml = decode_max_len(x, n_rows);
@@ -969,9 +910,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rpw_gu") {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
-  } else if (k == "rows_kernel") {
-    if (value != 4 && value != 5 && value != 7) MX_FAIL(x, MX_ERR_ARG, "rows_kernel must be 4, 5 or 7");
-    x->rows_kernel = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
@@ -984,22 +922,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;
-  } else if (k == "mega") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "mega must be 0 or 1");
-    x->mega = value;
-  } else if (k == "mega_trace") {
-    if (value && !x->mega_trace)
-      MX_TRY(x, x->alloc(&x->mega_trace, (size_t)MEGA_BLOCKS * x->c.layers * MEGA_TRACE_EV));
-    if (!value) x->mega_trace = nullptr;
-  } else if (k == "mega_ring") {
-    if (value != 8 && value != 16 && value != 32 && value != 48)
-      MX_FAIL(x, MX_ERR_ARG, "mega_ring must be 8, 16, 32 or 48");
-    if (x->mega_ok) {
-      int ok = 0;
-      MX_TRY(x, mega_resident(x->device, x->c.wdtype == WT_FP8 ? 1 : 0, value, &ok));
-      if (!ok) MX_FAIL(x, MX_ERR_STATE, "mega_ring: launch would not be co-resident");
-    }
-    x->mega_ring = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
     const bool any = value == 1 || value == 2 || value == 4;
     const bool wide = value == 3 || value == 6 || value == 8;  // 8-wave blocks only
@@ -1027,44 +949,26 @@ extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
   return MX_OK;
 }
 
-extern "C" int32_t* mx_llm_history(mx_llm* x) { return x ? x->hist_host : nullptr; }
-
-extern "C" int64_t mx_llm_mega_trace(mx_llm* x, int64_t* host_out, int64_t n) {
-  if (!x || !host_out) return MX_ERR_ARG;
-  if (!x->mega_trace) MX_FAIL(x, MX_ERR_STATE, "mega_trace option not enabled");
-  const int64_t total = (int64_t)MEGA_BLOCKS * x->c.layers * MEGA_TRACE_EV;
-  MX_TRY(x, hipSetDevice(x->device));
-  MX_TRY(x, hipDeviceSynchronize());
-  MX_TRY(x, hipMemcpy(host_out, x->mega_trace, (size_t)std::min(n, total) * 8,
-                      hipMemcpyDeviceToHost));
-  return std::min(n, total);
-}
-
-extern "C" int mx_llm_mega_info(mx_llm* x, int* eligible, int* status, void* stream) {
-  if (!x || !eligible || !status) return MX_ERR_ARG;
-  *eligible = x->mega && x->mega_ok ? 1 : 0;
-  *status = 0;
-  if (!x->mega_ok) return MX_OK;
-  MX_TRY(x, hipSetDevice(x->device));
-  MX_TRY(x, hipStreamSynchronize((hipStream_t)stream));
-  MX_TRY(x, hipMemcpy(status, x->mega_sync + x->c.layers * MEGA_SYNC_LAYER, 4,
-                      hipMemcpyDeviceToHost));
+extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next_pos) {
+  if (!x || !active || !next_pos || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
+  *active = x->row_active[row];
+  *next_pos = x->pos_mirror[row];
   return MX_OK;
 }
+
+extern "C" int32_t* mx_llm_history(mx_llm* x) { return x ? x->hist_host : nullptr; }
 
 extern "C" int mx_llm_debug_logits(mx_llm* x, int enable) {
   if (!x) return MX_ERR_ARG;
   if (!x->graphs.empty()) MX_FAIL(x, MX_ERR_STATE, "enable logits before the first decode");
-  MX_TRY(x, hipSetDevice(x->device));
-  if (enable && !x->logits_dbg) MX_TRY(x, x->alloc(&x->logits_dbg, (size_t)x->c.max_batch * x->c.vocab));
-  if (!enable) x->logits_dbg = nullptr;
+  x->logits_all = enable ? 1 : 0;
   return MX_OK;
 }
 
 extern "C" int mx_llm_read_logits(mx_llm* x, int row, float* host_out, void* stream) {
   if (!x || !host_out || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
-  if (!x->logits_dbg) MX_FAIL(x, MX_ERR_STATE, "logits not enabled");
-  MX_TRY(x, hipMemcpyAsync(host_out, x->logits_dbg + (size_t)row * x->c.vocab,
+  if (!x->logits_all) MX_FAIL(x, MX_ERR_STATE, "logits not enabled");
+  MX_TRY(x, hipMemcpyAsync(host_out, x->logits + (size_t)row * x->c.vocab,
                            (size_t)x->c.vocab * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   MX_TRY(x, hipStreamSynchronize((hipStream_t)stream));
   return MX_OK;
@@ -1240,8 +1144,8 @@ static void pick_tiles(ConvGemmArgs& g, int nphase) {
 }
 
 extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, int batch,
-                              const float* noise, uint64_t seed, int16_t* pcm, float* audio,
-                              int lo, int hi, void* stream) {
+                              const float* noise, uint64_t seed, const uint64_t* seeds,
+                              int16_t* pcm, float* audio, int lo, int hi, void* stream) {
   if (!s || !frames) return MX_ERR_ARG;
   if (!s->final) MX_FAIL(s, MX_ERR_STATE, "not finalized");
   if (n_frames < 1 || n_frames > s->max_frames || batch < 1 || batch > s->max_batch)
@@ -1262,7 +1166,7 @@ extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, i
   const int nlen = 3360 * n_frames;
   const float* nz = noise;
   if (!nz) {
-    MX_TRY(s, launch_gauss(s->noise, (int64_t)nlen * B, seed, st));
+    MX_TRY(s, launch_gauss(s->noise, (int64_t)nlen * B, seed, seeds, nlen, st));
     nz = s->noise;
   }
   const float* cb[3] = {W("q0.codebook"), W("q1.codebook"), W("q2.codebook")};

@@ -1,7 +1,5 @@
-// Multi-row decode GEMM, generation 4: the PRODUCT path (option "rows_kernel" = 4, default).
-// Same-process A/B at B = 4 / 8 (fp8) / 32 measured it 3.6-5 % faster per decode step than
-// generation 5 (llm_batched.hip, "rows_kernel" = 5), which is kept for its per-wave
-// straight-line streaming experiments.
+// Multi-row decode GEMM, generation 4 (the only multi-row generation built; generations 5
+// and 7 were measured 3.6-5 % and 13-60 % slower and were retired).
 // Multi-row decode / prefill projections on bf16 MFMA (gfx950) — the B = 2..64 path.
 //
 // Replaces the batched decode GEMMs of vLLM's engine (continuous batching of concurrent
@@ -117,14 +115,15 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
       } else if (EPI == EPI_ARGMAX) {
         const int slot = a.row_slot[b];
         const uint8_t* seen = a.seen + (size_t)slot * a.N;
-        const float pen = a.penalty[0];
+        const float pen = a.penalty[slot];
+        const bool keep = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int n = nb + i;
           if (n >= a.N) continue;
           float x = v[i];
           if (seen[n]) x = x > 0.f ? x / pen : x * pen;
-          if (a.logits) a.logits[(size_t)b * a.N + n] = x;
+          if (keep) a.logits[(size_t)b * a.N + n] = x;
           const unsigned long long key = argmax_key(x, (uint32_t)n);
           best[nt] = key > best[nt] ? key : best[nt];
         }

@@ -152,14 +152,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
         if (rt < nr) {
           const int slot = a.row_slot[r0 + rt];
           const uint8_t* seen = a.seen + (size_t)slot * a.N;
-          const float pen = a.penalty[0];
+          const float pen = a.penalty[slot];
+          const bool keep = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
 #pragma unroll
           for (int i = 0; i < RPW; ++i) {
             const int n = n0 + i;
             if (n < a.N) {
               float v = acc[i][rt];
               if (seen[n]) v = v > 0.f ? v / pen : v * pen;
-              if (a.logits && lane == 0) a.logits[(size_t)(r0 + rt) * a.N + n] = v;
+              if (keep && lane == 0) a.logits[(size_t)(r0 + rt) * a.N + n] = v;
               const unsigned long long key = argmax_key(v, (uint32_t)n);
               best[rt] = key > best[rt] ? key : best[rt];
             }
@@ -866,12 +867,7 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
-    if (a.rows_kernel == 7) {
-      const hipError_t e7 = launch_gemm_rows_v7(a, epi, norm, st);
-      if (e7 != hipErrorNotSupported) return e7;
-    }
-    const hipError_t e = a.rows_kernel != 5 ? v4::launch_gemm_rows_v4(a, epi, norm, st)
-                                            : launch_gemm_rows(a, epi, norm, st);
+    const hipError_t e = v4::launch_gemm_rows_v4(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
   }
   // RT = 1 for the decode batch of 1; RT = 4 otherwise (prefill / batched decode).

@@ -39,7 +39,6 @@ struct GemvArgs {
   int rows_pw_f8;          // the same for e4m3 weights
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
-  int rows_kernel;         // R >= 2 kernel generation: 4 (default), 7 (falls back to 4 outside its shapes), 5
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -51,9 +50,11 @@ struct GemvArgs {
   float* Q;                // [R][heads][128]
   // EPI_ARGMAX
   const uint8_t* seen;     // [slots][N]
-  const float* penalty;    // device scalar
+  const float* penalty;    // repetition penalty per KV slot [slots]
+  const float* samp_temp;  // sampling temperature per KV slot (> 0: the row samples)
   unsigned long long* best;  // [R]
-  float* logits;           // optional debug copy of penalised logits [R][N]
+  float* logits;           // penalised logits [R][N], kept for sampling rows (or every row)
+  int logits_all;          // 1: keep every row's logits (parity / debug reads)
 };
 
 struct AttnArgs {
@@ -88,64 +89,27 @@ struct CommitArgs {
   int scratch_slot;          // rows bound to this slot are parked: no advance, no history
 };
 
-// ---- persistent single-stream decode step (llm_mega.hip) --------------------------------
-// Fixed to the Orpheus-3B / Llama-3.2-3B shapes (hidden 3072, 24/8 heads of 128, FFN 8192).
-constexpr int MEGA_BLOCKS = 256;     // one block per CU, all resident
-constexpr int MEGA_SPLIT = 128;      // attention positions per split (one control wave)
-constexpr int MEGA_PART = 392;       // floats per split partial: acc[3][128], m[3], l[3], pad
-constexpr int MEGA_MAX_SPLITS = MEGA_BLOCKS / 8;  // longest fast-path context: 4096 positions
-// per-layer activation vectors (floats); each has its own lines, none is rewritten in a launch
-constexpr int MEGA_OFF_QKV = 0;      // q[24][128] | k[8][128] | v[8][128] (k, v bf16-exact)
-constexpr int MEGA_OFF_ATT = 5120;   // attention output [3072]
-constexpr int MEGA_OFF_HA = 8192;    // residual after attention [3072]
-constexpr int MEGA_OFF_ACT = 11264;  // SiLU(gate) * up [8192]
-constexpr int MEGA_OFF_HB = 19456;   // residual after the MLP [3072]
-constexpr int MEGA_WS_LAYER = 22528;
-// per-layer sync words (ints), zeroed by a memset node before every launch
-constexpr int MEGA_SYNC_Q = 0, MEGA_SYNC_O = 1, MEGA_SYNC_G = 2, MEGA_SYNC_D = 3;
-constexpr int MEGA_SYNC_TICK = 4;    // [8] split arrival tickets per kv head
-constexpr int MEGA_SYNC_DONE = 12;   // kv heads whose attention output is published
-constexpr int MEGA_SYNC_LAYER = 16;  // + one status word after the last layer (0 = ok)
-// sync words (+ status, padded to 16 B) are followed by the per-block seam flags
-inline size_t mega_sync_ints(int layers) { return ((size_t)layers * MEGA_SYNC_LAYER + 1 + 3) / 4 * 4; }
-inline size_t mega_flag_ints(int layers) { return (size_t)layers * 4 * MEGA_BLOCKS; }
-
-struct MegaArgs {
-  const void *wqkv, *wo, *wgu, *wd;  // [layers][packed rows][K] contiguous (bf16 or e4m3)
-  const float *sqkv, *so, *sgu, *sd; // fp8 row scales [layers][rows] (unused for bf16)
-  const float *attn_norm, *mlp_norm; // [layers][3072]
-  const float *rope_cos, *rope_sin;  // [max_pos][64]
-  const int32_t *row_slot, *row_pos; // decode row 0
-  uint16_t *kcache, *vcache;         // [layers][slots][8][max_pos][128], V^T per head
-  size_t kv_layer_elems;
-  int max_pos, layers, nsplit_cap;   // nsplit_cap: split partial slots per (layer, kv head)
-  int f8, ring;                      // e4m3 weights; register ring depth (8, 16, 32 or 48 units)
-  const float* h_in;                 // [3072] input embedding row (commit kernel output)
-  float* h_out;                      // [3072] residual after the last layer (lm_head input)
-  float* ws;                         // [layers][MEGA_WS_LAYER]
-  float* part;                       // [layers][8][nsplit_cap][MEGA_PART]
-  int* sync;                         // [layers][MEGA_SYNC_LAYER] + status
-  int* flags;                        // [layers][4 seams][256 blocks] arrival flags (same memset)
-  const void* dummy;                 // >= 128 KB of zeros: the ring's loads past the last layer
-  float eps, att_scale;
-  long long* trace;                  // diagnostics: [blocks][layers][MEGA_TRACE_EV] wall clocks, or null
-};
-constexpr int MEGA_TRACE_EV = 16;
-hipError_t launch_mega(const MegaArgs& a, hipStream_t st);
-hipError_t mega_resident(int device, int f8, int ring, int* ok);
 
 hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-// R >= 2 rows on bf16 MFMA (llm_batched.hip); hipErrorNotSupported if the shape is not covered
-hipError_t launch_gemm_rows(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-void gemm_rows_workspace(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
-namespace v4 {  // multi-row GEMM generation 4 (llm_batched_v4.hip): the default product path
+namespace v4 {  // multi-row GEMM on bf16 MFMA (llm_batched_v4.hip); NotSupported outside its shapes
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
 }  // namespace v4
-// R = 2..32 rows, one block per weight tile, K split over its waves (llm_batched_v7.hip);
-// hipErrorNotSupported outside the Orpheus-3B projection shapes
-hipError_t launch_gemm_rows_v7(const GemvArgs& a, int epi, bool norm, hipStream_t st);
+struct SampleArgs {
+  const float* logits;     // [R][V] penalised logits (kept by the lm_head epilogue)
+  const int32_t* row_slot; // [R]
+  const int32_t* row_pos;  // [R] position of the row's input token (RNG counter)
+  const float* temp;       // per KV slot: temperature (<= 0: greedy, kernel returns)
+  const float* top_p;      // per KV slot
+  const uint32_t* seed;    // per KV slot: Philox key (lo, hi)
+  unsigned long long* best;  // [R] argmax-key encoded token (read by commit)
+  int V;
+};
+hipError_t launch_sample(const SampleArgs& a, int R, hipStream_t st);
+hipError_t launch_set_slot_params(float* penalty, float* temp, float* top_p, uint32_t* seed,
+                                  int slot, float pen, float t, float p, uint64_t s,
+                                  hipStream_t st);
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);

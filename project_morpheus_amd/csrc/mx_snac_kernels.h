@@ -35,6 +35,7 @@ hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* 
 hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st);
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
                            int lo, int hi, float* audio, int16_t* pcm, hipStream_t st);
-hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, hipStream_t st);
+hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, const uint64_t* seeds, int64_t per,
+                        hipStream_t st);
 
 }  // namespace mx

@@ -331,10 +331,15 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
-__global__ void gauss_kernel(float* out, int64_t n, uint64_t seed) {
+// N(0,1) noise.  seeds == null: element i of the whole batch from `seed`; otherwise item
+// b = i / per draws element j = i % per from seeds[b], so a window's noise depends only on
+// its own seed (batching-invariant streams).
+__global__ void gauss_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* seeds,
+                             int64_t per) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t h = mix64(seed ^ mix64((uint64_t)i));
+  const uint64_t j = seeds ? (uint64_t)(i % per) : (uint64_t)i;
+  const uint64_t h = mix64((seeds ? seeds[i / per] : seed) ^ mix64(j));
   const float u1 = ((float)(h >> 40) + 1.0f) * (1.0f / 16777217.0f);
   const float u2 = (float)((h >> 16) & 0xffffff) * (1.0f / 16777216.0f);
   out[i] = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
@@ -390,9 +395,10 @@ hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int 
   return hipGetLastError();
 }
 
-hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, hipStream_t st) {
+hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, const uint64_t* seeds, int64_t per,
+                        hipStream_t st) {
   hipLaunchKernelGGL(gauss_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n,
-                     seed);
+                     seed, seeds, per);
   return hipGetLastError();
 }
 

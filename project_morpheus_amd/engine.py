@@ -80,23 +80,28 @@ class LlmEngine:
     def _check(self, rc):
         _lib.check(rc, self.lib.mx_llm_last_error, self.h)
 
-    def prefill(self, slot: int, row: int, ids: Sequence[int], penalty: float, stream) -> None:
+    def prefill(self, slot: int, row: int, ids: Sequence[int], penalty: float, stream, *,
+                temperature: float = 0.0, top_p: float = 1.0, seed: int = 0) -> None:
+        """Prefill ``ids`` into KV ``slot`` bound to decode ``row``; the slot decodes under
+        (penalty, temperature, top_p, seed) until the next prefill (temperature 0 = greedy)."""
         arr = np.ascontiguousarray(np.asarray(ids, dtype=np.int32))
+        sp = _lib.Sampling(temperature=float(temperature), top_p=float(top_p),
+                           repetition_penalty=float(penalty), seed=int(seed) & (2**64 - 1))
         self._check(self.lib.mx_llm_prefill(self.h, slot, row, arr.ctypes.data, len(arr),
-                                            penalty, C.c_void_p(stream.cuda_stream)))
+                                            C.byref(sp), C.c_void_p(stream.cuda_stream)))
 
-    def decode(self, n_rows: int, penalty: float, stream) -> None:
-        self._check(self.lib.mx_llm_decode(self.h, n_rows, penalty,
-                                           C.c_void_p(stream.cuda_stream)))
+    def decode(self, n_rows: int, stream) -> None:
+        """One step for rows [0, n_rows), each under its slot's generation parameters."""
+        self._check(self.lib.mx_llm_decode(self.h, n_rows, C.c_void_p(stream.cuda_stream)))
 
     PROFILE_CLASSES = ("qkv", "attention", "o_proj", "gate_up", "down", "lm_head", "commit")
 
-    def decode_profiled(self, n_rows: int, penalty: float, stream) -> Dict[str, float]:
+    def decode_profiled(self, n_rows: int, stream) -> Dict[str, float]:
         """One eager step with HIP events around every launch: ms per launch class
         (summed over layers) on the engine's own stream."""
         n = len(self.PROFILE_CLASSES)
         ms = (C.c_double * n)()
-        self._check(self.lib.mx_llm_decode_profiled(self.h, n_rows, penalty,
+        self._check(self.lib.mx_llm_decode_profiled(self.h, n_rows,
                                                     C.c_void_p(stream.cuda_stream), ms, n))
         return {k: ms[i] for i, k in enumerate(self.PROFILE_CLASSES)}
 
@@ -117,25 +122,6 @@ class LlmEngine:
                                                     C.byref(us)))
         return us.value
 
-    def mega_info(self, stream) -> Dict[str, int]:
-        """Persistent one-row step: eligible (used by one-row decode graphs) and the give-up
-        status of its last launch (0 = every in-launch hand-off completed)."""
-        el, st = C.c_int(0), C.c_int(0)
-        self._check(self.lib.mx_llm_mega_info(self.h, C.byref(el), C.byref(st),
-                                              C.c_void_p(stream.cuda_stream)))
-        return {"eligible": el.value, "status": st.value}
-
-    def mega_trace(self):
-        """Event clocks of the last persistent step (option mega_trace=1):
-        int64 [256 blocks][layers][16] at 100 MHz."""
-        import numpy as np
-        n = 256 * self.cfg.layers * 16
-        out = np.zeros(n, dtype=np.int64)
-        got = self.lib.mx_llm_mega_trace(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), n)
-        if got < 0:
-            _lib.check(int(got), self.lib.mx_llm_last_error, self.h)
-        return out.reshape(256, self.cfg.layers, 16)
-
     def set_option(self, key: str, value: int) -> None:
         self._check(self.lib.mx_llm_set_option(self.h, key.encode(), int(value)))
 
@@ -148,6 +134,12 @@ class LlmEngine:
         self._check(self.lib.mx_llm_read_logits(self.h, row, out.ctypes.data,
                                                 C.c_void_p(stream.cuda_stream)))
         return out
+
+    def row_state(self, row: int):
+        """(active, next position) of decode row ``row`` (host view)."""
+        a, p = C.c_int(0), C.c_int(0)
+        self._check(self.lib.mx_llm_row_state(self.h, row, C.byref(a), C.byref(p)))
+        return bool(a.value), p.value
 
     def release_row(self, row: int, stream) -> None:
         self._check(self.lib.mx_llm_release_row(self.h, row, C.c_void_p(stream.cuda_stream)))
@@ -191,10 +183,12 @@ class SnacDecoder:
         _lib.check(rc, self.lib.mx_snac_last_error, self.h)
 
     def decode_ptr(self, frames_ptr: int, n_frames: int, batch: int, noise_ptr: int, seed: int,
-                   pcm_ptr: int, audio_ptr: int, lo: int, hi: int, stream) -> None:
+                   pcm_ptr: int, audio_ptr: int, lo: int, hi: int, stream,
+                   seeds_ptr: int = 0) -> None:
+        """seeds_ptr: device-accessible uint64 [batch] noise seed per window (0: ``seed``)."""
         self._check(self.lib.mx_snac_decode(self.h, C.c_void_p(frames_ptr), n_frames, batch,
-                                            C.c_void_p(noise_ptr), seed, C.c_void_p(pcm_ptr),
-                                            C.c_void_p(audio_ptr), lo, hi,
+                                            C.c_void_p(noise_ptr), seed, C.c_void_p(seeds_ptr),
+                                            C.c_void_p(pcm_ptr), C.c_void_p(audio_ptr), lo, hi,
                                             C.c_void_p(stream.cuda_stream)))
 
     def decode(self, codes: torch.Tensor, noise: Optional[torch.Tensor] = None, seed: int = 0,
@@ -278,8 +272,10 @@ class Synthesizer:
     def run(self, prompt_ids: Sequence[int], max_tokens: int, penalty: float = 1.1,
             stop_ids: Sequence[int] = STOP_IDS, inject_ids: Optional[Sequence[int]] = None,
             stats: Optional[UtteranceStats] = None, slot: int = 0, row: int = 0,
-            noise_fn: Optional[Callable[[int], int]] = None) -> Iterator[bytes]:
-        """Prefill, then greedy-decode up to ``max_tokens`` tokens (engine_class.py:103-134).
+            temperature: float = 0.0, top_p: float = 1.0, seed: int = 0,
+            noise_seed: Optional[int] = None) -> Iterator[bytes]:
+        """Prefill, then decode up to ``max_tokens`` tokens (engine_class.py:103-134), greedy
+        unless ``temperature`` > 0.  Window j's SNAC noise is drawn from (noise_seed, j).
 
         ``inject_ids`` (bench / synthetic weights): token ids fed to the SNAC
         schedule in place of the model's own tokens; the LLM still decodes every step.
@@ -293,11 +289,14 @@ class Synthesizer:
         inflight: deque = deque()  # (token index, event)
         stop = set(int(s) for s in stop_ids)
 
-        llm.prefill(slot, row, prompt_ids, penalty, self.stream)
+        llm.prefill(slot, row, prompt_ids, penalty, self.stream, temperature=temperature,
+                    top_p=top_p, seed=seed)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         inflight.append((0, ev))
         launched, done, stopped = 1, 0, False
+        nseed = self.seed if noise_seed is None else noise_seed
+        widx = [0]  # windows of this utterance (noise stream index)
 
         def launch_window(win: List[int]):
             i = self._windows % self.ring.n
@@ -307,12 +306,13 @@ class Synthesizer:
             self.ring.codes[i][: 7 * nf] = win[: 7 * nf]
             lo, hi = SLICE_LO, min(SLICE_HI, SAMPLES_PER_FRAME * nf)
             self.snac.decode_ptr(self.ring.codes_dev[i], nf, 1, 0,
-                                 (self.seed * 1000003 + self._windows) & 0xFFFFFFFFFFFF,
+                                 (nseed * 1000003 + widx[0]) & 0xFFFFFFFFFFFF,
                                  self.ring.pcm_dev[i], 0, lo, max(lo, hi), self.snac_stream)
             e = torch.cuda.Event()
             e.record(self.snac_stream)
             pending.append((i, e, max(0, hi - lo) * 2))
             self._windows += 1
+            widx[0] += 1
             st.windows += 1
 
         def drain(block: bool, upto: Optional[int] = None):
@@ -331,31 +331,39 @@ class Synthesizer:
                         st.t_first_audio = time.perf_counter()
                     yield data
 
-        while done < max_tokens:
-            while (not stopped and launched < max_tokens and launched - done < self.depth):
-                llm.decode(1, penalty, self.stream)
-                e = torch.cuda.Event()
-                e.record(self.stream)
-                inflight.append((launched, e))
-                launched += 1
-            k, e = inflight.popleft()
-            e.synchronize()
-            tok = int(llm.hist[slot, n0 + k])
-            done += 1
-            st.tokens += 1
-            st.token_ids.append(tok)
-            feed = int(inject_ids[k]) if inject_ids is not None else tok
-            for win in sched.push(code_of_id(feed, sched.count)):
+        try:
+            while done < max_tokens:
+                while (not stopped and launched < max_tokens and launched - done < self.depth):
+                    llm.decode(1, self.stream)
+                    e = torch.cuda.Event()
+                    e.record(self.stream)
+                    inflight.append((launched, e))
+                    launched += 1
+                k, e = inflight.popleft()
+                e.synchronize()
+                tok = int(llm.hist[slot, n0 + k])
+                done += 1
+                st.tokens += 1
+                st.token_ids.append(tok)
+                feed = int(inject_ids[k]) if inject_ids is not None else tok
+                for win in sched.push(code_of_id(feed, sched.count)):
+                    yield from launch_window(win)
+                yield from drain(block=False)
+                if tok in stop:
+                    stopped = True
+                    break
+            for win in sched.flush():
                 yield from launch_window(win)
-            yield from drain(block=False)
-            if tok in stop:
-                stopped = True
-                break
-        # drain speculative steps still in flight (their tokens are discarded)
-        for _, e in inflight:
-            e.synchronize()
-        for win in sched.flush():
-            yield from launch_window(win)
-        yield from drain(block=True)
-        llm.release_row(row, self.stream)
-        st.t_end = time.perf_counter()
+            yield from drain(block=True)
+        finally:
+            # normal end, error or the consumer closing the generator (barge-in): wait for
+            # the speculative steps and the SNAC calls still queued (their results are
+            # dropped), then give the row back -- the slot is free for the next utterance
+            for _, e in inflight:
+                e.synchronize()
+            for _, e, _ in pending:
+                e.synchronize()
+            pending.clear()
+            llm.release_row(row, self.stream)
+            self.stream.synchronize()
+            st.t_end = time.perf_counter()

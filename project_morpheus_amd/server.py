@@ -64,9 +64,15 @@ def build_app(adapter_cls=MxTTSAdapter) -> Starlette:
                               use_batching=len(payload.input) > 1000, max_batch_chars=1000)
 
         async def body():
-            yield riff_header()
-            async for pcm in adapter_pcm(adapter):
-                yield pcm
+            done = False
+            try:
+                yield riff_header()
+                async for pcm in adapter_pcm(adapter):
+                    yield pcm
+                done = True
+            finally:
+                if not done:  # client went away: cancel the GPU stream, free its row
+                    await adapter.reset()
 
         return StreamingResponse(body(), media_type="audio/wav")
 
@@ -83,10 +89,14 @@ def build_app(adapter_cls=MxTTSAdapter) -> Starlette:
                 await websocket.close(code=1008)
                 return
             voice = I.resolve_voice(websocket.query_params.get("voice") or I.DEFAULT_VOICE)
-            await websocket.send_bytes(riff_header())
-            async for pcm in adapter_pcm(adapter_cls(prompt, voice)):
-                await websocket.send_bytes(pcm)
-            await websocket.close()
+            adapter = adapter_cls(prompt, voice)
+            try:
+                await websocket.send_bytes(riff_header())
+                async for pcm in adapter_pcm(adapter):
+                    await websocket.send_bytes(pcm)
+                await websocket.close()
+            finally:
+                await adapter.reset()  # no-op after a complete stream; cancels otherwise
         except WebSocketDisconnect:
             pass
 

@@ -66,11 +66,11 @@ def main():
             for r in range(R):
                 llm.prefill(r, r, prompt, 1.1, st)
             for _ in range(args.pos - len(prompt)):
-                llm.decode(R, 1.1, st)
+                llm.decode(R, st)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(args.reps):
-                llm.decode(R, 1.1, st)
+                llm.decode(R, st)
             e1.record(st)
             e1.synchronize()
             res[name].append(round(e0.elapsed_time(e1) / args.reps, 4))

@@ -58,16 +58,16 @@ def main():
     for i in range(P):
         llm.prefill(i, i, prompt, 1.1, st)
     for _ in range(args.pos - len(prompt)):
-        llm.decode(P, 1.1, st)
+        llm.decode(P, st)
     prof = {}
     n = 8
     for _ in range(n):
-        for k, v in llm.decode_profiled(P, 1.1, st).items():
+        for k, v in llm.decode_profiled(P, st).items():
             prof[k] = prof.get(k, 0.0) + v / n
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(20):
-        llm.decode(P, 1.1, st)
+        llm.decode(P, st)
     e1.record(st)
     e1.synchronize()
     print(json.dumps({"profile_rows": P, "pos": args.pos,

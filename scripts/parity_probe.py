@@ -25,7 +25,7 @@ def run(cfg, w, prompts, steps, legacy):
         eng.prefill(r, r, p, 1.1, st)
     for k in range(steps):
         if k > 0:
-            eng.decode(B, 1.1, st)
+            eng.decode(B, st)
         st.synchronize()
         for r, p in enumerate(prompts):
             logits[r].append(eng.read_logits(r, st))

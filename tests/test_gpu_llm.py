@@ -47,11 +47,9 @@ def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512, options=None, info=Non
     eng.prefill(slot, 0, prompt, penalty, st)
     for k in range(steps):
         if k > 0:
-            eng.decode(1, penalty, st)
+            eng.decode(1, st)
         logits.append(eng.read_logits(0, st))
         toks.append(int(eng.hist[slot, len(prompt) + k]))
-    if info is not None:
-        info.update(eng.mega_info(st))
     eng.close()
     return toks, logits
 
@@ -116,47 +114,6 @@ def _orpheus_prompt(n_text, seed):
         + [128009, 128260, 128261, 128257]
 
 
-def test_mega_step_is_used_and_completes():
-    """Option mega=1 at Orpheus widths: the one-row step runs as ONE persistent launch
-    (llm_mega.hip; off by default); its
-    in-launch hand-offs all completed (status 0) and it matches the oracle."""
-    cfg = _cfgs("orpheus2")
-    w = synthetic_llm_weights(cfg, seed=5)
-    info = {}
-    assert _compare(cfg, w, _orpheus_prompt(12, 6), 20, options={"mega": 1}, info=info) >= 16
-    assert info == {"eligible": 1, "status": 0}
-
-
-def test_mega_three_layers_attention_splits():
-    """3 layers (two layer seams of the weight ring plus the tail), prompt of 230 ids and 60
-    steps: the context crosses 256, so the persistent step runs 2 then 3 attention splits per
-    kv head with the last-arriver merge, and the new position moves across split edges."""
-    cfg = C.OrpheusConfig(layers=3)
-    w = synthetic_llm_weights(cfg, seed=7)
-    info = {}
-    assert _compare(cfg, w, _orpheus_prompt(226, 8), 60, options={"mega": 1}, info=info) >= 45
-    assert info == {"eligible": 1, "status": 0}
-
-
-def test_mega_matches_multi_kernel_step():
-    """Persistent step vs the per-kernel step on the same weights and prompt: penalised logits
-    agree to the same tolerance the oracle comparison uses, token for token."""
-    cfg = _cfgs("orpheus2")
-    w = synthetic_llm_weights(cfg, seed=9)
-    prompt = _orpheus_prompt(40, 10)
-    i1, i0 = {}, {}
-    t1, l1 = _run_gpu(cfg, w, prompt, 16, 1.1, options={"mega": 1}, info=i1)
-    t0, l0 = _run_gpu(cfg, w, prompt, 16, 1.1, options={"mega": 0}, info=i0)
-    assert i1["eligible"] == 1 and i1["status"] == 0 and i0["eligible"] == 0
-    for k in range(16):
-        np.testing.assert_allclose(l1[k], l0[k], atol=LOGIT_TOL, rtol=LOGIT_TOL,
-                                   err_msg=f"step {k}")
-        if t1[k] != t0[k]:
-            top2 = np.sort(l0[k])[-2:]
-            assert top2[1] - top2[0] < TIE_MARGIN
-            break  # histories diverge after a near-tie flip
-
-
 def test_bad_args_fail_loudly():
     from project_morpheus_amd import _lib
     from project_morpheus_amd.engine import LlmEngine
@@ -169,7 +126,7 @@ def test_bad_args_fail_loudly():
     with pytest.raises(_lib.MxError):
         eng.prefill(0, 0, [cfg.vocab], 1.1, st)        # id outside the vocabulary
     with pytest.raises(_lib.MxError):
-        eng.decode(2, 1.1, st)                          # more rows than max_batch
+        eng.decode(2, st)                          # more rows than max_batch
     bad = dict(w)
     bad.pop("l1.wd")
     with pytest.raises(_lib.MxError):
@@ -194,7 +151,7 @@ def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=N
         eng.prefill(r, r, p, penalty, st)
     for k in range(steps):
         if k > 0:
-            eng.decode(B, penalty, st)
+            eng.decode(B, st)
         st.synchronize()
         for r, p in enumerate(prompts):
             logits[r].append(eng.read_logits(r, st))
@@ -259,23 +216,66 @@ def test_batched_decode_orpheus_width_4_rows():
     assert _compare_rows(cfg, w, prompts, 10) >= 0.8 * 4 * 10
 
 
-def test_batched_decode_orpheus_width_20_rows_gen7():
-    """20 streams at Orpheus widths through the generation-7 multi-row GEMM (option
-    rows_kernel=7: one block per 16-row weight tile, K over its 8 / 16 waves, 32-row batch
-    tiles) for qkv / o / gate-up / down / lm_head; ragged prompts."""
-    cfg = _cfgs("orpheus2")
-    w = synthetic_llm_weights(cfg, seed=21)
-    rng = np.random.default_rng(22)
-    prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 4 + 2 * i)]
-               + [128009, 128260, 128261, 128257] for i in range(20)]
-    assert _compare_rows(cfg, w, prompts, 6, options={"rows_kernel": 7}) >= 0.8 * 20 * 6
+def _orpheus_prompts(n, seed, base=4, step=2):
+    rng = np.random.default_rng(seed)
+    return [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, base + step * i)]
+            + [128009, 128260, 128261, 128257] for i in range(n)]
 
 
-def test_batched_decode_orpheus_width_gen4():
-    """The default multi-row generation (rows_kernel=4) at Orpheus widths, 6 rows."""
+def test_batched_decode_orpheus_width_6_rows():
+    """The multi-row GEMM at Orpheus widths, 6 rows (one 16-row batch tile)."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=23)
-    rng = np.random.default_rng(24)
-    prompts = [[128259, 128000] + [int(x) for x in rng.integers(1000, 128000, 6 + i)]
-               + [128009, 128260, 128261, 128257] for i in range(6)]
-    assert _compare_rows(cfg, w, prompts, 6, options={"rows_kernel": 4}) >= 0.8 * 6 * 6
+    assert _compare_rows(cfg, w, _orpheus_prompts(6, 24, 6, 1), 6) >= 0.8 * 6 * 6
+
+
+def test_batched_decode_orpheus_width_32_rows():
+    """configs[2]'s shape: 32 rows at Orpheus widths (two 16-row batch tiles per weight tile,
+    the kernels bench.py times for B = 32), ragged prompts."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=21)
+    assert _compare_rows(cfg, w, _orpheus_prompts(32, 22, 4, 1), 5) >= 0.8 * 32 * 5
+
+
+def test_batched_decode_orpheus_width_64_rows():
+    """64 rows at Orpheus widths: four 16-row batch tiles (the largest tile class)."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=25)
+    assert _compare_rows(cfg, w, _orpheus_prompts(64, 26, 3, 1), 3) >= 0.8 * 64 * 3
+
+
+def test_full_depth_orpheus_3b_single_stream():
+    """configs[1]'s exact model: all 28 layers at Orpheus-3B widths (6.6 GB of bf16 weights,
+    the 156,940-entry tied lm_head), one stream, teacher-forced against the fp32 oracle on
+    the host (13 GB of fp32 weights).
+
+    Tolerance at full depth: the bf16-KV rounding flips behind LOGIT_TOL (module docstring)
+    compound over 28 layers; measured on MI355X the worst logit is 6.3e-3 off (6 of 156,940
+    entries above 5e-3) at step 0.  Bound: |d| <= 1.5e-2 + 1.5e-2 |x| per entry, mean |d| <=
+    1e-3, tokens tie-aware with a 3e-2 margin."""
+    cfg = C.OrpheusConfig()
+    w = synthetic_llm_weights(cfg, seed=0, device="cuda")
+    prompt = _orpheus_prompt(24, 31)
+    steps = 10
+    g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, 1.1, max_pos=256)
+    wc = {k: v.cpu() for k, v in w.items()}
+    del w
+    torch.cuda.empty_cache()
+    ref = L.LlamaRef(_ref_cfg(cfg), wc, max_pos=256)
+    del wc
+    _, r_logits = L.greedy_generate(ref, prompt, steps, 1.1, return_logits=True, forced=g_toks)
+    agree, worst = 0, 0.0
+    for k in range(steps):
+        rl = r_logits[k].numpy()
+        d = np.abs(g_logits[k] - rl)
+        worst = max(worst, float(d.max()))
+        np.testing.assert_allclose(g_logits[k], rl, atol=1.5e-2, rtol=1.5e-2,
+                                   err_msg=f"logits step {k}")
+        assert float(d.mean()) <= 1e-3, f"step {k}: mean |d| {d.mean():.2e}"
+        if g_toks[k] != int(np.argmax(rl)):
+            top2 = np.sort(rl)[-2:]
+            assert top2[1] - top2[0] < 3e-2, f"step {k}"
+        else:
+            agree += 1
+    print(f"28-layer parity: worst |d logit| {worst:.2e}, argmax agreement {agree}/{steps}")
+    assert agree >= 8

@@ -1,0 +1,88 @@
+"""GPU temperature + top-p sampling (csrc/sample_kernels.hip) vs oracle/sampling_ref.py.
+
+The sampled token of every step must equal the oracle's draw from the SAME penalised logits
+(read back from the GPU) at the same Philox counter; the only accepted difference is a
+near-tie of the exponential race (relative score margin < 1e-5: expf/logf last-ulp
+differences between the device and numpy).  The logits themselves are checked against the
+LLM oracle, teacher-forced, with the tolerances of tests/test_gpu_llm.py; a greedy row with
+its own repetition penalty runs in the same batch (per-slot generation parameters).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import llama_ref as L
+from oracle import sampling_ref as S
+from project_morpheus_amd import config as C
+from project_morpheus_amd.weights import synthetic_llm_weights
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 5e-3
+RACE_MARGIN = 1e-5
+
+
+def _run(cfg, w, rows, steps):
+    """rows: [(prompt, penalty, temperature, top_p, seed)] -> per row (tokens, logits)."""
+    from project_morpheus_amd.engine import LlmEngine
+    B = len(rows)
+    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=256, max_batch=B, max_prefill=64)
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    out = [([], []) for _ in rows]
+    for r, (p, pen, t, tp, sd) in enumerate(rows):
+        eng.prefill(r, r, p, pen, st, temperature=t, top_p=tp, seed=sd)
+    for k in range(steps):
+        if k:
+            eng.decode(B, st)
+        st.synchronize()
+        for r, (p, *_rest) in enumerate(rows):
+            out[r][1].append(eng.read_logits(r, st))
+            out[r][0].append(int(eng.hist[r, len(p) + k]))
+    eng.close()
+    return out
+
+
+def _check(cfg, w, rows, steps):
+    out = _run(cfg, w, rows, steps)
+    rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                     kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
+    ref = L.LlamaRef(rc, w, max_pos=256)
+    exact = 0
+    for r, (p, pen, t, tp, sd) in enumerate(rows):
+        toks, logits = out[r]
+        _, rl = L.greedy_generate(ref, p, steps, pen, return_logits=True, forced=toks)
+        for k in range(steps):
+            np.testing.assert_allclose(logits[k], rl[k].numpy(), atol=LOGIT_TOL, rtol=LOGIT_TOL,
+                                       err_msg=f"row {r} step {k}")
+            want, margin = S.sample(logits[k], t, tp, sd, len(p) - 1 + k, return_margin=True)
+            if toks[k] == want:
+                exact += 1
+            else:
+                assert margin < RACE_MARGIN, f"row {r} step {k}: {toks[k]} vs {want}"
+    return exact
+
+
+@pytest.mark.parametrize("std", [0.05, 0.5])
+def test_sampling_matches_oracle_full_vocab(std):
+    """Orpheus vocabulary (156,940 ids) on a narrow model: std 0.05 gives flat logits (the
+    nucleus holds most of the vocabulary), std 0.5 peaked ones (a handful of ids)."""
+    cfg = C.OrpheusConfig(hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024)
+    w = synthetic_llm_weights(cfg, seed=61, std=std, norm_jitter=0.5)
+    rng = np.random.default_rng(62)
+    p0 = [int(x) for x in rng.integers(0, cfg.vocab, 11)]
+    p1 = [int(x) for x in rng.integers(0, cfg.vocab, 7)]
+    p2 = [int(x) for x in rng.integers(0, cfg.vocab, 5)]
+    rows = [(p0, 1.1, 0.6, 0.9, 1234567),          # the reference defaults (inference.py:75-105)
+            (p1, 1.3, 0.0, 1.0, 0),                # greedy row, its own penalty
+            (p2, 1.1, 1.0, 1.0, 2**40 + 17)]       # plain temperature sampling, no nucleus cut
+    steps = 12
+    assert _check(cfg, w, rows, steps) >= 3 * steps - 2
+
+
+def test_sampling_single_row_path():
+    """B = 1: the single-row lm_head GEMV keeps the logits for the sampler."""
+    cfg = C.OrpheusConfig(hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024, vocab=5000)
+    w = synthetic_llm_weights(cfg, seed=63, std=0.2, norm_jitter=0.5)
+    p = [int(x) for x in np.random.default_rng(64).integers(0, cfg.vocab, 9)]
+    assert _check(cfg, w, [(p, 1.1, 0.6, 0.8, 99)], 16) >= 15

@@ -150,3 +150,43 @@ def test_adapter_reset_restarts_and_clears():
     assert b.pcm == b"\x01\x00" * 8 + b"\x02\x00" * 8 and b.eos
     assert c.pcm == b"" and c.eos
     assert calls == ["p", "p"]
+
+
+def test_adapter_reset_does_not_wedge_the_producer():
+    """a producer far ahead of the puller (> queue size) must not block
+    forever after reset(); a second adapter still completes."""
+    import asyncio
+    import threading
+
+    from project_morpheus_amd.adapter import MxTTSAdapter
+
+    closed = threading.Event()
+
+    class Busy(MxTTSAdapter):
+        @staticmethod
+        def source(prompt, voice, use_batching, max_batch_chars, cancel):
+            try:
+                for i in range(500):
+                    yield bytes([i % 256]) * 100
+            finally:
+                closed.set()
+
+    async def go():
+        a = Busy("x")
+        c = await a.pull(100)
+        assert len(c.pcm) == 100
+        await asyncio.sleep(0.3)  # producer fills the 64-entry queue and waits
+        t = a._thread
+        await a.reset()
+        t.join(timeout=5)
+        assert not t.is_alive() and closed.is_set()
+        b = Busy("y")
+        total = 0
+        while True:
+            ch = await b.pull(4096)
+            total += len(ch.pcm)
+            if ch.eos:
+                break
+        return total
+
+    assert asyncio.run(go()) == 500 * 100
