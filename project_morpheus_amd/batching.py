@@ -66,6 +66,8 @@ class StreamRequest:
     noise_seed: Optional[int] = None        # SNAC noise stream (None: assigned at admission)
     on_chunk: Optional[Callable[["StreamRequest", bytes], None]] = None
     on_done: Optional[Callable[["StreamRequest"], None]] = None
+    on_token: Optional[Callable[["StreamRequest", int], None]] = None
+    audio: bool = True                      # False: token stream only (no SNAC windows)
     # filled in by the synthesizer
     tokens: List[int] = field(default_factory=list)
     pcm: List[bytes] = field(default_factory=list)  # for callers that collect chunks here
@@ -162,6 +164,13 @@ class StreamHandle:
         self.req.cancel()
 
 
+class TokenHandle(StreamHandle):
+    """Online token-only stream (the /v1/completions surface): ``get`` -> token id | None."""
+
+    def _token(self, req, tok: int) -> None:
+        self._q.put(tok)
+
+
 class BatchSynthesizer:
     def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: int = 2, seed: int = 0):
         if llm.max_slots < llm.max_batch:
@@ -223,8 +232,10 @@ class BatchSynthesizer:
     def submit(self, req: StreamRequest) -> StreamHandle:
         if self._thread is None:
             self.start()
-        h = StreamHandle(req)
+        h = StreamHandle(req) if req.audio else TokenHandle(req)
         req.on_chunk, req.on_done = h._chunk, h._done
+        if not req.audio:
+            req.on_token = h._token
         req.arrival = time.perf_counter() - self._t0
         with self._cv:
             if self._stop:
@@ -377,7 +388,7 @@ class BatchSynthesizer:
 
         def finish(r: _Row, due: List):
             req = r.req
-            if not req.cancelled:
+            if not req.cancelled and req.audio:
                 for win in r.sched.flush():
                     due.append((req, req.windows, win))
                     req.windows += 1
@@ -433,10 +444,13 @@ class BatchSynthesizer:
                     continue  # speculative step of a stream that already ended
                 tok = int(llm.hist[r.idx, r.n0 + k])
                 req.tokens.append(tok)
-                feed = int(req.inject_ids[k]) if req.inject_ids is not None else tok
-                for win in r.sched.push(code_of_id(feed, r.sched.count)):
-                    due.append((req, req.windows, win))
-                    req.windows += 1
+                if req.on_token is not None:
+                    req.on_token(req, tok)
+                if req.audio:
+                    feed = int(req.inject_ids[k]) if req.inject_ids is not None else tok
+                    for win in r.sched.push(code_of_id(feed, r.sched.count)):
+                        due.append((req, req.windows, win))
+                        req.windows += 1
                 if tok in req.stop_ids or len(req.tokens) >= r.limit:
                     r.stopped = True
             for r in rows:

@@ -5,6 +5,7 @@
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -29,24 +30,35 @@ def _obj(s: str) -> str:
     return os.path.join(OBJ_DIR, s.replace(".hip", ".o"))
 
 
-def _deps_mtime() -> float:
-    deps = [os.path.join(CSRC, h) for h in HEADERS]
-    deps.append(os.path.join(HERE, "..", "include", "morpheus_mx.h"))
-    return max(os.path.getmtime(d) for d in deps if os.path.exists(d))
+def _includes(path: str, seen=None) -> set:
+    """Local headers a source includes, transitively (#include "...")."""
+    seen = set() if seen is None else seen
+    try:
+        text = open(path).read()
+    except OSError:
+        return seen
+    for m in re.finditer(r'#include\s+"([^"]+)"', text):
+        h = os.path.normpath(os.path.join(os.path.dirname(path), m.group(1)))
+        if h not in seen:
+            seen.add(h)
+            _includes(h, seen)
+    return seen
 
 
-def _stale(s: str, hdr: float) -> bool:
+def _stale(s: str, hdr=None) -> bool:
     o = _obj(s)
-    return not os.path.exists(o) or os.path.getmtime(o) < max(
-        hdr, os.path.getmtime(os.path.join(CSRC, s)))
+    if not os.path.exists(o):
+        return True
+    src = os.path.join(CSRC, s)
+    deps = [src] + [h for h in _includes(src) if os.path.exists(h)]
+    return os.path.getmtime(o) < max(os.path.getmtime(d) for d in deps)
 
 
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
-    hdr = _deps_mtime()
     t = os.path.getmtime(LIB)
-    return any(_stale(s, hdr) or os.path.getmtime(_obj(s)) > t for s in SOURCES)
+    return any(_stale(s) or os.path.getmtime(_obj(s)) > t for s in SOURCES)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -55,10 +67,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return LIB
     os.makedirs(OBJ_DIR, exist_ok=True)
-    hdr = _deps_mtime()
     procs = []
     for s in SOURCES:
-        if not force and not _stale(s, hdr):
+        if not force and not _stale(s):
             continue
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                "-munsafe-fp-atomics", "-Wno-unused-result", "-x", "hip", "-c",

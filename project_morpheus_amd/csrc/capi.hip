@@ -116,7 +116,7 @@ struct mx_llm {
   bool final = false;
   int max_rows = 0;
   int legacy_gemv = 0;          // option: grid-stride GEMV for R = 1 too (A/B timing)
-  int att_cpw_b1 = 1;           // option: 32-position chunks per wave, single-row attention
+  int att_cpw_b1 = 0;           // option: chunks per wave, single-row attention (0 = auto)
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
@@ -483,8 +483,29 @@ static int att_cpw_pick(int want, int nw) {
   if (want <= 4) return want < 1 ? 1 : want;
   return want <= 6 ? 6 : 8;
 }
+// One-row steps: the o-proj prologue merges at most 8 split partials (gemv1 NSM), so the
+// split is the shortest of 128 / 256 / 512 (4 waves x 1 / 2 / 4 chunks) or 1024 / 2048
+// positions (8 waves x 4 / 8 chunks) that covers the context in <= 8 splits.
+static void att_b1_shape(const mx_llm* x, int max_len, int* nw, int* cpw) {
+  if (x->att_cpw_b1 > 0) {  // option override (4-wave blocks)
+    *nw = x->att_nw_b1;
+    *cpw = x->att_cpw_b1;
+    return;
+  }
+  static const int shapes[5][2] = {{4, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
+  for (const auto& sh : shapes) {
+    *nw = sh[0];
+    *cpw = sh[1];
+    if ((max_len + 32 * sh[0] * sh[1] - 1) / (32 * sh[0] * sh[1]) <= 8) return;
+  }
+}
+
 static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
-  if (R == 1) return x->att_cpw_b1;
+  if (R == 1) {
+    int nw = 4, cpw = 1;
+    att_b1_shape(x, max_len, &nw, &cpw);
+    return cpw;
+  }
   if (x->att_cpw_batch > 0) return x->att_cpw_batch;
   const int nw = x->att_nw_batch;
   const int pairs = R * x->c.kv_heads;
@@ -500,6 +521,8 @@ struct RowSet {
   int R;
   int max_len;  // upper bound of any row's position + 1 (sizes the attention grid)
   int cpw;      // attention chunks per wave (att_cpw_auto)
+  int nw;       // attention waves per block
+  int nsplit;   // attention splits of the launch (grid x)
 };
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
@@ -558,8 +581,10 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
     at.scale = 1.0f / sqrtf(128.0f);
     at.cpw = rs.cpw;
-    at.nw = rs.R == 1 ? x->att_nw_b1 : x->att_nw_batch;
+    at.nw = rs.nw;
     at.split_stride = c.max_pos / ATT_S_MIN;
+    const bool b1_merge = rs.R == 1 && !x->legacy_gemv && rs.nsplit <= 8;
+    at.no_merge = b1_merge ? 1 : 0;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
     at.out = x->att;
     PROF_BEGIN(PK_ATTN);
@@ -571,6 +596,11 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     attach_ws(x, o);
     o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
+    if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
+      o.att_ml = x->part_ml; o.att_acc = x->part_acc; o.att_S = 32 * rs.nw * rs.cpw;
+      o.att_stride = at.split_stride; o.att_nsm = rs.nsplit; o.heads = c.heads;
+      o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
+    }
     PROF_BEGIN(PK_O);
     e = launch_gemv(o, EPI_RESID, false, st);
     PROF_END();
@@ -626,10 +656,20 @@ static int decode_max_len(const mx_llm* x, int n_rows) {
   return m;
 }
 
+static int att_nw_of(const mx_llm* x, int R, int max_len) {
+  if (R != 1) return x->att_nw_batch;
+  int nw = 4, cpw = 1;
+  att_b1_shape(x, max_len, &nw, &cpw);
+  return nw;
+}
+
 static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hipStream_t st,
                                  Prof* prof) {
   const auto& c = x->c;
-  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw};
+  const int nw = att_nw_of(x, n_rows, max_len);
+  const int S = 32 * nw * cpw;
+  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw, nw,
+            (max_len + S - 1) / S};
   hipError_t e = enqueue_layers(x, rs, st, prof);
   PROF_BEGIN(PK_HEAD);
   if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, x->row_pos, n_rows, x->best, st);
@@ -669,7 +709,9 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, launch_set_rows(x->pre_slot, x->pre_pos, n, slot, 0, st));
   MX_TRY(x, launch_embed_rows(x->pre_ids, n, slot, x->embed, c.hidden, c.vocab, x->seen,
                               x->h_pre, st));
-  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n, att_cpw_auto(x, n, n)};
+  RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n, att_cpw_auto(x, n, n),
+            att_nw_of(x, n, n), 0};
+  rs.nsplit = (n + 32 * rs.nw * rs.cpw - 1) / (32 * rs.nw * rs.cpw);
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
   MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1),
@@ -709,11 +751,13 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   MX_TRY(x, hipSetDevice(x->device));
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
-  const int cpw = att_cpw_auto(x, n_rows, decode_max_len(x, n_rows));
-  const int S = 32 * cpw * (n_rows == 1 ? x->att_nw_b1 : x->att_nw_batch);
-  const int nsplit = (decode_max_len(x, n_rows) + S - 1) / S;
-  // (the chunk count is part of the key: one nsplit can come from two chunk counts)
-  const int key = (n_rows * 16 + cpw) * 4096 + nsplit;
+  const int ml = decode_max_len(x, n_rows);
+  const int cpw = att_cpw_auto(x, n_rows, ml);
+  const int nw = att_nw_of(x, n_rows, ml);
+  const int S = 32 * cpw * nw;
+  const int nsplit = (ml + S - 1) / S;
+  // (chunks and waves are part of the key: one nsplit can come from several shapes)
+  const int key = ((n_rows * 16 + cpw) * 16 + nw) * 4096 + nsplit;
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
@@ -923,10 +967,10 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;
   } else if (k == "att_cpw" || k == "att_cpw_batch") {
-    const bool any = value == 1 || value == 2 || value == 4;
+    const bool any = value == 1 || value == 2 || value == 4 || (value == 0 && k == "att_cpw");
     const bool wide = value == 3 || value == 6 || value == 8;  // 8-wave blocks only
     if (!(any || (wide && k == "att_cpw_batch") || (value == 0 && k == "att_cpw_batch")))
-      MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 1, 2 or 4 (att_cpw_batch also 3/6/8, 0 = auto)");
+      MX_FAIL(x, MX_ERR_ARG, "att_cpw must be 0 (auto), 1, 2 or 4 (att_cpw_batch also 3/6/8, 0 = auto)");
     (k == "att_cpw" ? x->att_cpw_b1 : x->att_cpw_batch) = value;
   } else {
     MX_FAIL(x, MX_ERR_ARG, "unknown option " + k);

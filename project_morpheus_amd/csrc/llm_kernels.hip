@@ -247,7 +247,54 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
 // ---------------------------------------------------------------------------------
 // F8: weights are OCP e4m3 bytes with one fp32 scale per row (16 weights per 16-byte load,
 // converted in registers by v_cvt_pk_f32_fp8 -- exact), else bf16 (8 per load).
-template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8>
+// MRG (NSM > 0, the R = 1 o-projection): the activation is the attention output, merged
+// here from its split partials (attn_kernel no_merge mode): for 8-dim group j of head hh,
+// att = sum_s e^(m_s - M) acc_s / sum_s e^(m_s - M) l_s over the row's live splits (at most
+// NSM).  The partial loads go out first, the weight loads behind them, and the merge runs
+// under the weight latency -- the split merge costs no extra launch, ticket or round trip.
+template <int NSM>
+struct MergeIn {  // one 8-dim group's split partials, loaded
+  float2 ml[NSM];
+  float4 lo[NSM], hi[NSM];
+};
+template <int NSM>
+__device__ __forceinline__ void merge_load(const GemvArgs& a, int j, int ns, MergeIn<NSM>& in) {
+  const int GRP = a.heads / a.kv_heads;
+  const int hh = j >> 4, d0 = (j & 15) * 8;
+  const int kvh = hh / GRP, hin = hh - kvh * GRP;
+  const size_t pb = (size_t)kvh * a.att_stride;
+#pragma unroll
+  for (int s = 0; s < NSM; ++s) {
+    const size_t sp = pb + min(s, ns - 1);
+    in.ml[s] = *reinterpret_cast<const float2*>(a.att_ml + (sp * GRP + hin) * 2);
+    const float4* ac = reinterpret_cast<const float4*>(a.att_acc + (sp * GRP + hin) * 128 + d0);
+    in.lo[s] = ac[0];
+    in.hi[s] = ac[1];
+  }
+}
+template <int NSM>
+__device__ __forceinline__ void merge_apply(const MergeIn<NSM>& in, int ns, float* x) {
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < NSM; ++s)
+    if (s < ns) M = fmaxf(M, in.ml[s].x);
+  float den = 0.f;
+  float num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NSM; ++s) {
+    const float f = s < ns ? expf(in.ml[s].x - M) : 0.f;
+    den = fmaf(f, in.ml[s].y, den);
+    num[0] = fmaf(f, in.lo[s].x, num[0]); num[1] = fmaf(f, in.lo[s].y, num[1]);
+    num[2] = fmaf(f, in.lo[s].z, num[2]); num[3] = fmaf(f, in.lo[s].w, num[3]);
+    num[4] = fmaf(f, in.hi[s].x, num[4]); num[5] = fmaf(f, in.hi[s].y, num[5]);
+    num[6] = fmaf(f, in.hi[s].z, num[6]); num[7] = fmaf(f, in.hi[s].w, num[7]);
+  }
+  const float inv = 1.0f / den;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = num[i] * inv;
+}
+
+template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8, int NSM = 0>
 __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   constexpr int NT = WPB * 64;
   constexpr int EPC = F8 ? 16 : 8;             // weights per 16-byte chunk
@@ -267,13 +314,22 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   const float4* X4 = reinterpret_cast<const float4*>(a.X);
   const float4* NW4 = reinterpret_cast<const float4*>(a.norm_w);
   float4 xv[XPT][PL], nv[XPT][PL];
+  constexpr int NG = KC * EPC / 8;  // 8-dim groups of the merged activation (MRG)
+  int ns = 1;
+  MergeIn<(NSM > 0 ? NSM : 1)> mi;
+  if constexpr (NSM > 0) {
+    const int L = a.row_pos[0] + 1;
+    ns = (L + a.att_S - 1) / a.att_S;
+    merge_load<NSM>(a, min(tid, NG - 1), ns, mi);  // group tid's partial loads go first
+  } else {
 #pragma unroll
-  for (int i = 0; i < XPT; ++i) {
-    const int m = min(tid + i * NT, KC - 1);
+    for (int i = 0; i < XPT; ++i) {
+      const int m = min(tid + i * NT, KC - 1);
 #pragma unroll
-    for (int q = 0; q < PL; ++q) {
-      xv[i][q] = X4[PL * m + q];
-      if (NORM) nv[i][q] = NW4[PL * m + q];
+      for (int q = 0; q < PL; ++q) {
+        xv[i][q] = X4[PL * m + q];
+        if (NORM) nv[i][q] = NW4[PL * m + q];
+      }
     }
   }
   float res[RPW], wsc[RPW];
@@ -295,6 +351,18 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   __builtin_amdgcn_sched_barrier(0);
 
   // 3. prologue under the weight latency
+  if constexpr (NSM > 0) {
+    // merged 8-dim group j -> chunk m = 8j / EPC, planes q0, q0 + 1 of the staged layout
+    for (int j = tid; j < NG; j += NT) {
+      if (j != tid) merge_load<NSM>(a, j, ns, mi);
+      float xm[8];
+      merge_apply<NSM>(mi, ns, xm);
+      const int m = (8 * j) / EPC, q0 = ((8 * j) % EPC) / 4;
+      xs[q0 * KC + m] = make_float4(xm[0], xm[1], xm[2], xm[3]);
+      xs[(q0 + 1) * KC + m] = make_float4(xm[4], xm[5], xm[6], xm[7]);
+    }
+    __syncthreads();
+  }
   float scale = 1.f;
   if (NORM) {
     float ss = 0.f;
@@ -316,7 +384,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
     scale = 1.0f / sqrtf(tot / (float)(KC * EPC) + a.eps);
   }
 #pragma unroll
-  for (int i = 0; i < XPT; ++i) {
+  for (int i = 0; i < XPT && NSM == 0; ++i) {
     const int m = tid + i * NT;
     if (m < KC) {
 #pragma unroll
@@ -635,6 +703,22 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
     }
   }
   float* out = a.out + ((size_t)r * a.heads + kvh * GRP) * 128;
+  if (a.no_merge) {  // one-row step: the o-proj GEMV merges the splits in its prologue
+    const size_t pb = ((size_t)r * a.kv_heads + kvh) * a.split_stride + split;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int idx = tid + NT * k;
+      if (idx < GRP * 128) {
+        const int h = idx >> 7, td = idx & 127;
+        a.part_acc[(pb * GRP + h) * 128 + td] = bn[k];
+        if (td == 0) {
+          a.part_ml[(pb * GRP + h) * 2] = bm[k];
+          a.part_ml[(pb * GRP + h) * 2 + 1] = bl[k];
+        }
+      }
+    }
+    return;
+  }
   if (nsplit == 1) {
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -823,6 +907,19 @@ static int gemv_blocks(int N, int rpw, int ytiles, int target) {
 template <int KCH, int RPW, int EPI, bool NORM, bool F8>
 static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
   const int G = a.N / RPW;
+  if constexpr (EPI == EPI_RESID && !NORM && (F8 ? (KCH == 1 || KCH == 3)
+                                                 : (KCH == 1 || KCH == 2 || KCH == 6))) {
+    if (a.att_ml) {  // R = 1 o-projection with the attention split merge (8-wave blocks)
+      const int ns = a.att_nsm;
+      if (ns > 8 || (KCH * 64 * (F8 ? 16 : 8)) / 8 > 512) return hipErrorInvalidValue;
+      const dim3 grid((G + 7) / 8), blk(512);
+      if (ns <= 2) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8, 2>), grid, blk, 0, st, a);
+      else if (ns <= 4) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8, 4>), grid, blk, 0, st, a);
+      else hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8, 8>), grid, blk, 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  if (a.att_ml) return hipErrorNotSupported;
   if (a.wpb == 8)
     hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8>), dim3((G + 7) / 8), dim3(512), 0, st, a);
   else
@@ -858,7 +955,7 @@ static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   if (a.R == 1 && epi != EPI_ARGMAX && !a.force_legacy) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
-    if (e != hipErrorNotSupported) return e;
+    if (e != hipErrorNotSupported || a.att_ml) return e;  // (the merge has no other kernel)
   }
   // fp8 single-row lm_head: the grid-stride argmax GEMV with e4m3 weights
   if (a.R == 1 && epi == EPI_ARGMAX && norm && a.wdtype == WT_FP8 && a.K % 1024 == 0) {

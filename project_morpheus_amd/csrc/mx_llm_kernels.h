@@ -48,6 +48,11 @@ struct GemvArgs {
   uint16_t* vcache;
   int heads, kv_heads, max_pos;
   float* Q;                // [R][heads][128]
+  // R = 1 o-proj: merge the attention split partials in the prologue (attn no_merge mode)
+  const float* att_ml;     // [kv_heads][att_stride][grp][2]  (m, l) per split, row 0
+  const float* att_acc;    // [kv_heads][att_stride][grp][128]
+  int att_S, att_stride;   // split length (positions) and partial slots per kv head
+  int att_nsm;             // splits the launch may have to merge (host bound, <= 8)
   // EPI_ARGMAX
   const uint8_t* seen;     // [slots][N]
   const float* penalty;    // repetition penalty per KV slot [slots]
@@ -73,6 +78,7 @@ struct AttnArgs {
   int* counter;            // [R][kv_heads] split arrival tickets (zero between launches)
   float* out;              // [R][heads*128]
   int debug;               // timing experiments only (0 in the product path)
+  int no_merge;            // 1: every split stores its partial, the consumer merges (R = 1)
 };
 
 struct CommitArgs {

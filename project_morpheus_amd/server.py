@@ -52,7 +52,19 @@ async def adapter_pcm(adapter) -> "AsyncIterator[bytes]":
             return
 
 
-def build_app(adapter_cls=MxTTSAdapter) -> Starlette:
+def _service_tokens(prompt_ids, **params):
+    from .service import get_service
+    return get_service().submit_tokens(prompt_ids, **params)
+
+
+def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=None,
+              decode=None) -> Starlette:
+    """``token_source(prompt_ids, **params)`` backs /v1/completions (default: this GPU's
+    service); ``encode`` / ``decode`` default to the process tokenizer."""
+    from .completions import build_route
+    from .tokenizer import default_tokenizer
+    if encode is None:
+        encode = lambda s: default_tokenizer().encode(s)  # noqa: E731
     async def speech(request: Request) -> StreamingResponse:
         try:
             payload = SpeechRequest(**await request.json())
@@ -101,6 +113,8 @@ def build_app(adapter_cls=MxTTSAdapter) -> Starlette:
             pass
 
     return Starlette(routes=[Route("/v1/audio/speech", speech, methods=["POST"]),
+                             Route("/v1/completions", build_route(token_source, encode, decode),
+                                   methods=["POST"]),
                              Route("/v1/audio/voices", voices, methods=["GET"]),
                              WebSocketRoute("/ws/tts", tts_ws)])
 

@@ -89,6 +89,18 @@ class Service:
             req.stop_ids = ()  # synthetic weights decode the full budget (bench contract)
         return self.batch.submit(req)
 
+    def submit_tokens(self, prompt_ids, max_tokens: Optional[int] = None,
+                      temperature: Optional[float] = None, top_p: Optional[float] = None,
+                      penalty: float = I.REPETITION_PENALTY, seed: Optional[int] = None):
+        """Token-only stream (completions surface): a TokenHandle of generated ids."""
+        ids = list(prompt_ids)
+        key = zlib.crc32(np.asarray(ids, dtype=np.int32).tobytes()) if seed is None else seed
+        req = StreamRequest(prompt_ids=ids, max_tokens=max_tokens or I.MAX_TOKENS,
+                            penalty=penalty,
+                            temperature=I.TEMPERATURE if temperature is None else temperature,
+                            top_p=I.TOP_P if top_p is None else top_p, seed=key, audio=False)
+        return self.batch.submit(req)
+
     def stream(self, text: str, voice: str = I.DEFAULT_VOICE, max_tokens: Optional[int] = None,
                penalty: float = I.REPETITION_PENALTY, stats=None,
                cancel: Optional[threading.Event] = None, **kw) -> Iterator[bytes]:

@@ -5,7 +5,9 @@ The sampled token of every step must equal the oracle's draw from the SAME penal
 near-tie of the exponential race (relative score margin < 1e-5: expf/logf last-ulp
 differences between the device and numpy).  The logits themselves are checked against the
 LLM oracle, teacher-forced, with the tolerances of tests/test_gpu_llm.py; a greedy row with
-its own repetition penalty runs in the same batch (per-slot generation parameters).
+its own repetition penalty runs in the same batch (per-slot generation parameters).  The
+logit tolerance scales with the logits' spread (the std-0.5 weights give logits ~10x larger
+than the std-0.05 ones the 5e-3 bound was measured on).
 """
 import numpy as np
 import pytest
@@ -53,7 +55,9 @@ def _check(cfg, w, rows, steps):
         toks, logits = out[r]
         _, rl = L.greedy_generate(ref, p, steps, pen, return_logits=True, forced=toks)
         for k in range(steps):
-            np.testing.assert_allclose(logits[k], rl[k].numpy(), atol=LOGIT_TOL, rtol=LOGIT_TOL,
+            want_l = rl[k].numpy()
+            tol = LOGIT_TOL * max(1.0, float(np.std(want_l)))  # scaled with the logits
+            np.testing.assert_allclose(logits[k], want_l, atol=tol, rtol=LOGIT_TOL,
                                        err_msg=f"row {r} step {k}")
             want, margin = S.sample(logits[k], t, tp, sd, len(p) - 1 + k, return_margin=True)
             if toks[k] == want:
