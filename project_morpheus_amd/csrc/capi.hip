@@ -119,7 +119,8 @@ struct mx_llm {
   int att_cpw_b1 = 0;           // option: chunks per wave, single-row attention (0 = auto)
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
-  int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
+  int att_nw_b1 = 4, att_nw_batch = 8;
+  int o_merge = 1;  // option: one-row o-proj merges the attention splits (0 = ticket merge)  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
   int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
@@ -583,7 +584,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.cpw = rs.cpw;
     at.nw = rs.nw;
     at.split_stride = c.max_pos / ATT_S_MIN;
-    const bool b1_merge = rs.R == 1 && !x->legacy_gemv && rs.nsplit <= 8;
+    const bool b1_merge = rs.R == 1 && !x->legacy_gemv && x->o_merge && rs.nsplit <= 8;
     at.no_merge = b1_merge ? 1 : 0;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
     at.out = x->att;
@@ -954,6 +955,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rpw_gu") {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
+  } else if (k == "o_merge") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "o_merge must be 0 or 1");
+    x->o_merge = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;

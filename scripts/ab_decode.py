@@ -14,26 +14,24 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULTS = {"legacy_gemv": 0, "att_cpw": 1, "att_cpw_batch": 1, "att_nw": 4, "att_nw_batch": 8, "gemv_wpb": 4, "rpw_o": 0,
-            "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0, "rows_npart": 0, "rows_kernel": 4}
+DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
+            "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_dbg": 0,
+            "rows_npart": 0, "o_merge": 1}
 VARIANTS = {
     "base": {},
-    "rows_v5": {"rows_kernel": 5},
-    "att_b_nw4cpw2": {"att_nw_batch": 4, "att_cpw_batch": 2},
-    "att_cpw2": {"att_cpw": 2},
-    "att_cpw4": {"att_cpw": 4},
+    "ticket": {"o_merge": 0, "att_cpw": 1},
+    "rpw_o2": {"rpw_o": 2},
+    "cpw2": {"att_cpw": 2},
+    "cpw2_rpw_o2": {"att_cpw": 2, "rpw_o": 2},
     "rpw_gu4": {"rpw_gu": 4},
-    "att_cpw_batch1": {"att_cpw_batch": 1},
-    "rows_contig": {"rows_dbg": 4},
-    "rows_nostage": {"rows_dbg": 2},
-    "rows_np2": {"rows_npart": 2},
-    "att_cpw_batch4": {"att_cpw_batch": 4},
+    "rpw_down2": {"rpw_down": 2},
+    "wpb8": {"gemv_wpb": 8},
 }
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pos", type=int, default=1200)
+    ap.add_argument("--pos", default="300,600,1100")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=",".join(VARIANTS))
@@ -57,29 +55,32 @@ def main():
     st = torch.cuda.Stream()
     prompt = list(range(1000, 1020))
     names = args.variants.split(",")
-    res = {n: [] for n in names}
+    positions = [int(p) for p in str(args.pos).split(",")]
+    res = {(n, p): [] for n in names for p in positions}
     for rnd in range(args.rounds):
         for name in names:
             opts = dict(DEFAULTS, **VARIANTS[name])
             for k, v in opts.items():
                 llm.set_option(k, v)
-            for r in range(R):
-                llm.prefill(r, r, prompt, 1.1, st)
-            for _ in range(args.pos - len(prompt)):
-                llm.decode(R, st)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(args.reps):
-                llm.decode(R, st)
-            e1.record(st)
-            e1.synchronize()
-            res[name].append(round(e0.elapsed_time(e1) / args.reps, 4))
-            for r in range(R):
-                llm.release_row(r, st)
-            st.synchronize()
-        print(f"round {rnd}: " + json.dumps({n: res[n][-1] for n in names}), flush=True)
-    print(json.dumps({n: {"median_ms": statistics.median(v), "all": v} for n, v in res.items()},
-                     indent=1))
+            for pos in positions:
+                for r in range(R):
+                    llm.prefill(r, r, prompt, 1.1, st)
+                for _ in range(pos - len(prompt)):
+                    llm.decode(R, st)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(args.reps):
+                    llm.decode(R, st)
+                e1.record(st)
+                e1.synchronize()
+                res[(name, pos)].append(round(e0.elapsed_time(e1) / args.reps, 4))
+                for r in range(R):
+                    llm.release_row(r, st)
+                st.synchronize()
+        print(f"round {rnd}: " + json.dumps({f"{n}@{p}": res[(n, p)][-1]
+                                            for n in names for p in positions}), flush=True)
+    for n in names:
+        print(n, {p: statistics.median(res[(n, p)]) for p in positions}, flush=True)
 
 
 if __name__ == "__main__":
