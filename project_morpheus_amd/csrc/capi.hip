@@ -598,6 +598,8 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
     if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
+      if (o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step faster
+                                  // than 1 row per wave (fewer partial re-reads)
       o.att_ml = x->part_ml; o.att_acc = x->part_acc; o.att_S = 32 * rs.nw * rs.cpw;
       o.att_stride = at.split_stride; o.att_nsm = rs.nsplit; o.heads = c.heads;
       o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
