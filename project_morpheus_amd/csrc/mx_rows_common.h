@@ -1,0 +1,150 @@
+// Shared pieces of the multi-row (R >= 2) decode GEMMs: activation part split, the MFMA-tile
+// epilogues (RoPE + KV append, residual, SiLU*up, penalty + argmax), write-through partials.
+#pragma once
+#include "mx_common.h"
+#include "mx_llm_kernels.h"
+
+namespace mx {
+namespace rows {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// x[0..7] -> NPART bf16x8 fragments with x = sum of parts (to fp32 rounding for NPART 3)
+template <int NPART>
+__device__ __forceinline__ void split_parts(float* x, bf16x8* f) {
+#pragma unroll
+  for (int p = 0; p < NPART; ++p) {
+    uint32_t wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t pk = pack2_bf16(x[2 * j], x[2 * j + 1]);
+      wv[j] = pk;
+      if (p + 1 < NPART) {  // residual for the next part (exact in fp32)
+        x[2 * j] -= bf16_lo(pk);
+        x[2 * j + 1] -= bf16_hi(pk);
+      }
+    }
+    f[p] = __builtin_bit_cast(bf16x8, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+  }
+}
+
+// Epilogue of one wave's tile: lane (batch col c, group g) holds weight rows
+// n0 + 16 mt + 4 g + i for batch rows r0 + 16 nt + c (MFMA C/D layout).
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT][NT],
+                                              const float (&scale)[NT], int n0, int r0, int c,
+                                              int g) {
+  unsigned long long best[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) best[nt] = 0ull;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int b = r0 + 16 * nt + c;
+    const bool bok = b < a.R;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int nb = n0 + 16 * mt + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] * scale[nt];
+      if (a.wdtype == WT_FP8) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] *= a.wscale[min(nb + i, a.N - 1)];
+      }
+      if (!bok || nb >= a.N) continue;
+      if (EPI == EPI_STORE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.Y[(size_t)b * a.ystride + nb + i] = v[i];
+      } else if (EPI == EPI_RESID) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.Y[(size_t)b * a.ystride + nb + i] += v[i];
+      } else if (EPI == EPI_SILU) {
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const float gt = v[i], up = v[i + 1];
+          a.Y[(size_t)b * (a.N >> 1) + ((nb + i) >> 1)] = gt / (1.0f + expf(-gt)) * up;
+        }
+      } else if (EPI == EPI_QKV) {
+        const int slot = a.row_slot[b], pos = a.row_pos[b];
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int n = nb + i;
+          const int hh = n >> 7, within = n & 127, p = within >> 1;
+          const float x1 = v[i], x2 = v[i + 1];
+          if (hh < a.heads + a.kv_heads) {
+            const float cs = a.rope_cos[(size_t)pos * 64 + p];
+            const float sn = a.rope_sin[(size_t)pos * 64 + p];
+            const float o1 = x1 * cs - x2 * sn;
+            const float o2 = x2 * cs + x1 * sn;
+            if (hh < a.heads) {
+              float* q = a.Q + ((size_t)b * a.heads + hh) * 128;
+              q[p] = o1;
+              q[p + 64] = o2;
+            } else {
+              uint16_t* kc = a.kcache +
+                  (((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos + pos) * 128;
+              kc[p] = f32_to_bf16(o1);
+              kc[p + 64] = f32_to_bf16(o2);
+            }
+          } else {
+            uint16_t* vc = a.vcache +
+                ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
+            vc[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
+            vc[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
+          }
+        }
+      } else if (EPI == EPI_ARGMAX) {
+        const int slot = a.row_slot[b];
+        const uint8_t* seen = a.seen + (size_t)slot * a.N;
+        const float pen = a.penalty[slot];
+        const bool keep = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = nb + i;
+          if (n >= a.N) continue;
+          float x = v[i];
+          if (seen[n]) x = x > 0.f ? x / pen : x * pen;
+          if (keep) a.logits[(size_t)b * a.N + n] = x;
+          const unsigned long long key = argmax_key(x, (uint32_t)n);
+          best[nt] = key > best[nt] ? key : best[nt];
+        }
+      }
+    }
+  }
+  if (EPI == EPI_ARGMAX) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      unsigned long long k = best[nt];
+#pragma unroll
+      for (int m = 16; m <= 32; m <<= 1) {
+        const unsigned long long o = __shfl_xor(k, m, 64);
+        k = o > k ? o : k;
+      }
+      const int b = r0 + 16 * nt + c;
+      if (g == 0 && b < a.R && k) atomicMax(a.best + b, k);
+    }
+  }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte write-through (sc1) store / load of a partial-tile quad (MI355X_MICROARCH.md
+// "Valid forms" row 1 with 16-B accesses)
+__device__ __forceinline__ void st4_wt(float* base, size_t idx, const f32x4& v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(idx * 4), 0, 16);
+}
+__device__ __forceinline__ f32x4 ld4_wt(const float* base, size_t idx) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace rows
+}  // namespace mx

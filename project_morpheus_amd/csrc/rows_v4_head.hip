@@ -1,0 +1,22 @@
+// Multi-row decode GEMM generation 4, EPI_ARGMAX / EPI_STORE instantiations (own translation unit).
+#include "mx_rows_v4.inc"
+
+namespace mx {
+namespace v4 {
+
+hipError_t launch_rows_head(const GemvArgs& a, int epi, bool norm, int nt, hipStream_t st) {
+#define MX_R(EPI_, NORM_)                                                                 \
+  if (epi == EPI_ && norm == NORM_) {                                                     \
+    if (nt == 1) return launch_rows_k<1, 1, EPI_, NORM_>(a, st);                          \
+    if (nt == 2) return launch_rows_k<1, 2, EPI_, NORM_>(a, st);                          \
+    return launch_rows_k<1, 4, EPI_, NORM_>(a, st);                                       \
+  }
+  MX_R(EPI_ARGMAX, true)
+  MX_R(EPI_STORE, false)
+  MX_R(EPI_STORE, true)
+#undef MX_R
+  return hipErrorNotSupported;
+}
+
+}  // namespace v4
+}  // namespace mx
