@@ -127,7 +127,6 @@ struct mx_llm {
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
-  int rows_gen = 8;                  // option: multi-row layer projections, generation 8 or 4
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
@@ -248,12 +247,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
         v4::gemm_rows_workspace_v4(sh[0], sh[1], std::min(r, sh[2]), sh[3], &wf, &tk);
         x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
         x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
-        if (sh[3] != EPI_ARGMAX)  // generation 8 plans per row count (every count <= max)
-          for (int rr = 2; rr <= std::min(r, sh[2]); ++rr) {
-            g8::workspace(sh[0], sh[1], rr, f8, &wf, &tk);
-            x->rows_ws_floats = std::max(x->rows_ws_floats, wf);
-            x->rows_tickets_n = std::max(x->rows_tickets_n, tk);
-          }
       }
   }
   A(x->rows_ws, std::max<size_t>(x->rows_ws_floats, 1));
@@ -311,7 +304,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
     e = hipMemcpy(x->row_pos, zero.data(), c.max_batch * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->cap, hipStreamNonBlocking);
   if (e == hipSuccess) e = gemv_prepare(std::max(std::max(c.hidden, c.ffn), c.heads * 128));
-  if (e == hipSuccess) e = g8::prepare();
   if (e != hipSuccess) {
     (void)hipGetLastError();
     g_err = std::string("init failed: ") + hipGetErrorString(e);
@@ -540,7 +532,6 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
-  g.rows_gen = x->rows_gen;
   g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -966,9 +957,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rpw_gu") {
     if (value != 0 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rpw_gu must be 0, 2 or 4");
     x->rpw_gu = value;
-  } else if (k == "rows_gen") {
-    if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "rows_gen must be 4 or 8");
-    x->rows_gen = value;
   } else if (k == "o_merge") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "o_merge must be 0 or 1");
     x->o_merge = value;

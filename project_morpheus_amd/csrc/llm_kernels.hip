@@ -964,10 +964,6 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
-    if (a.rows_gen != 4 && a.R >= 2 && epi != EPI_ARGMAX) {
-      const hipError_t e8 = g8::launch(a, epi, norm, st);
-      if (e8 != hipErrorNotSupported) return e8;
-    }
     const hipError_t e = v4::launch_gemm_rows_v4(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;
   }

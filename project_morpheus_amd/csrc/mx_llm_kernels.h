@@ -39,7 +39,6 @@ struct GemvArgs {
   int rows_pw_f8;          // the same for e4m3 weights
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
-  int rows_gen;            // multi-row layer projections: 8 (default) or 4
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -99,12 +98,7 @@ struct CommitArgs {
 
 hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-namespace g8 {  // multi-row GEMM generation 8 (mx_rows_g8.inc): the layer projections
-hipError_t prepare();
-hipError_t launch(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-void workspace(int N, int K, int R, bool f8, size_t* ws_floats, size_t* tickets);
-}  // namespace g8
-namespace v4 {  // multi-row GEMM generation 4 (mx_rows_v4.inc): lm_head / argmax, option rows_gen=4
+namespace v4 {  // multi-row GEMM generation 4 (mx_rows_v4.inc)
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
 }  // namespace v4
