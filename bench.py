@@ -171,7 +171,7 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
             "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
 
 
-def run_http(args, syn, prompt_text, inject, local):
+def run_http(args, syn, prompt_text, inject, local, orchestrated=False):
     """configs[1] at the HTTP level: one ``POST /v1/audio/speech`` through the ASGI app of
     ``project_morpheus_amd.server`` (no sockets; the app's own adapter and streaming body),
     the adapter's source bound to this process's engine.  RTF = audio / wall from request
@@ -197,7 +197,8 @@ def run_http(args, syn, prompt_text, inject, local):
                     return
                 yield pcm
 
-    app = build_app(adapter_cls=BenchAdapter)
+    orchs = []
+    app = build_app(adapter_cls=BenchAdapter, orchestrated=orchestrated, orchestrators=orchs)
 
     async def one():
         body = _json.dumps({"input": prompt_text, "voice": "tara"}).encode()
@@ -229,9 +230,17 @@ def run_http(args, syn, prompt_text, inject, local):
     pcm = sum(n for _, n in marks) - 44
     first = next(t for t, n in marks[1:] if n > 0) if len(marks) > 1 else t0
     wall = marks[-1][0] - t0
-    return {"workload": "configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream)",
-            "value": round(pcm / 2 / 24000.0 / wall, 3), "unit": "audio-sec/wall-sec",
-            "first_audio_ms": round(1e3 * (first - t0), 2), "bytes": pcm}
+    first_pcm = next((t for t, n in marks[1:] if n > 0), t0)
+    out = {"workload": ("configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream)"
+                        + (", reference Orchestrator contract: ChunkLadder byte pulls (8-64), "
+                           "per-pull JSON/base64 log, stitch_chunks, WAV streamer"
+                           if orchestrated else ", 4096-byte pulls")),
+           "value": round(pcm / 2 / 24000.0 / wall, 3), "unit": "audio-sec/wall-sec",
+           "first_audio_ms": round(1e3 * (first_pcm - t0), 2), "bytes": pcm}
+    if orchestrated and orchs:
+        out["pulls"] = orchs[-1].pulls
+        out["mean_pull_bytes"] = round(pcm / max(1, orchs[-1].pulls), 2)
+    return out
 
 
 def run_long_read(args, llm, snac, rank, world, dist):
@@ -392,9 +401,10 @@ def main():
         firsts = [x for r in fl for x in r]
 
     # ---- configs[1] at the HTTP level (rank 0 only: one request through the ASGI app) ----
-    http_level = None
+    http_level = http_orch = None
     if rank == 0 and not args.no_http:
         http_level = run_http(args, syn, "Hello world", inject, local)
+        http_orch = run_http(args, syn, "Hello world", inject, local, orchestrated=True)
 
     # ---- configs[2]: B concurrent streams per GPU, continuous batching + batched SNAC ----
     batched = None
@@ -466,6 +476,7 @@ def main():
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
             "audio_seconds": round(audio, 3),
             "http_level": http_level,
+            "http_level_orchestrator": http_orch,
             "configs_2_batched": batched,
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,

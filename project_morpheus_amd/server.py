@@ -58,9 +58,11 @@ def _service_tokens(prompt_ids, **params):
 
 
 def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=None,
-              decode=None) -> Starlette:
+              decode=None, orchestrated: bool = False, orchestrators=None) -> Starlette:
     """``token_source(prompt_ids, **params)`` backs /v1/completions (default: this GPU's
-    service); ``encode`` / ``decode`` default to the process tokenizer."""
+    service); ``encode`` / ``decode`` default to the process tokenizer.  ``orchestrated``:
+    /v1/audio/speech runs the reference's Orchestrator contract (ladder pulls of 8-64 bytes,
+    per-pull JSON/base64 log, stitcher; orchestrator.py) instead of 4096-byte pulls."""
     from .completions import build_route
     from .tokenizer import default_tokenizer
     if encode is None:
@@ -79,7 +81,12 @@ def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=Non
             done = False
             try:
                 yield riff_header()
-                async for pcm in adapter_pcm(adapter):
+                if orchestrated:
+                    from .orchestrator import orchestrated_pcm_stream
+                    pcm_iter = orchestrated_pcm_stream(adapter, orchestrators)
+                else:
+                    pcm_iter = adapter_pcm(adapter)
+                async for pcm in pcm_iter:
                     yield pcm
                 done = True
             finally:

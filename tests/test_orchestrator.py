@@ -1,0 +1,78 @@
+"""The restated Orchestrator contract (project_morpheus_amd/orchestrator.py) on CPU: the
+ladder starts at 8 and steps by buffer depth (chunk_ladder.py:10-60), every pull is logged
+with its base64 PCM (core.py:97-104), PCM arrives intact through stitch_chunks and the WAV
+streamer, and barge-in resets the adapter."""
+import asyncio
+import base64
+
+from starlette.testclient import TestClient
+
+from project_morpheus_amd.adapter import MxTTSAdapter
+from project_morpheus_amd.orchestrator import ChunkLadder, Orchestrator, PlaybackBuffer
+from project_morpheus_amd.server import build_app, riff_header
+
+PCM = [bytes(range(256)) * 8, b"", bytes(range(100)), bytes(range(200)) * 3]
+
+
+class Fake(MxTTSAdapter):
+    @staticmethod
+    def source(prompt, voice, use_batching, max_batch_chars, cancel):
+        yield from PCM
+
+
+def test_ladder_adapt():
+    lad = ChunkLadder()
+    assert lad.current == 8
+    lad.adapt(10.0, (50.0, 250.0))
+    assert lad.current == 12
+    lad.adapt(300.0, (50.0, 250.0))
+    assert lad.current == 8
+    lad.adapt(300.0, (50.0, 250.0))
+    assert lad.current == 8
+
+
+def test_orchestrator_pulls_log_and_pcm():
+    events = []
+
+    async def go():
+        o = Orchestrator(Fake("x"), PlaybackBuffer(1000))
+        out = [c async for c in o.stream(on_event=events.append)]
+        return o, out
+
+    o, out = asyncio.run(go())
+    pcm = b"".join(c.pcm for c in out)
+    assert pcm == b"".join(PCM)
+    assert out[-1].eos and o.pulls == len(events)
+    assert b"".join(base64.b64decode(e["pcm"]) for e in events) == pcm
+    windows = [e["token_window"] for e in events]
+    assert windows[0] == 8 and max(windows) <= 64 and min(windows) >= 8
+
+
+def test_barge_in_resets_adapter():
+    class Counting(Fake):
+        resets = 0
+
+        async def reset(self):
+            Counting.resets += 1
+            await super().reset()
+
+    async def go():
+        o = Orchestrator(Counting("x"), PlaybackBuffer(1000))
+        n = 0
+        async for _ in o.stream():
+            n += 1
+            if n == 3:
+                o.signal_barge_in()
+        return o
+
+    o = asyncio.run(go())
+    assert Counting.resets == 1 and o.timeline[-1]["stage"] == "barge_in_reset"
+
+
+def test_orchestrated_speech_route():
+    orchs = []
+    app = build_app(adapter_cls=Fake, orchestrated=True, orchestrators=orchs)
+    r = TestClient(app).post("/v1/audio/speech", json={"input": "Hello", "voice": "tara"})
+    assert r.status_code == 200
+    assert r.content == riff_header() + b"".join(PCM)
+    assert orchs and orchs[0].pulls >= len(b"".join(PCM)) // 64
