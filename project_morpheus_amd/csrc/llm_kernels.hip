@@ -958,9 +958,11 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     if (e != hipErrorNotSupported || a.att_ml) return e;  // (the merge has no other kernel)
   }
   // fp8 single-row lm_head: the grid-stride argmax GEMV with e4m3 weights
+  // (8 rows per wave: an e4m3 row is 3 KB, so 4 rows left a wave only 12 loads of 16 B in
+  // flight; measured 106.8 us = 4.5 TB/s at 4 rows)
   if (a.R == 1 && epi == EPI_ARGMAX && norm && a.wdtype == WT_FP8 && a.K % 1024 == 0) {
-    const int blocks = gemv_blocks(a.N, 4, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
-    return launch_gemv_t<1, 4, EPI_ARGMAX, true, true>(a, blocks, st);
+    const int blocks = gemv_blocks(a.N, 8, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
+    return launch_gemv_t<1, 8, EPI_ARGMAX, true, true>(a, blocks, st);
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
@@ -1007,7 +1009,7 @@ hipError_t gemv_prepare(int kmax) {
   MX_A(4, 2, EPI_QKV, true) MX_A(4, 4, EPI_ARGMAX, true)
 #undef MX_A
   if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 4, EPI_ARGMAX, true, true>),
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 8, EPI_ARGMAX, true, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
   return e;
 }

@@ -26,16 +26,30 @@ struct ConvGemmArgs {
   int wk, nsub;         // waves splitting K; 16-column subtiles per tile
 };
 
+// Per-call I/O of a graph-captured window decode: the captured kernels read these from a
+// ctx-owned device copy (written by set_io before each replay), so one graph serves every
+// call of its shape.  Eager launches pass io = nullptr and use their direct arguments.
+struct SnacIO {
+  const int32_t* frames;
+  const uint64_t* seeds;
+  uint64_t seed;
+  int16_t* pcm;
+  float* audio;
+};
+hipError_t launch_set_io(SnacIO* dst, const SnacIO& v, hipStream_t st);
+
 hipError_t launch_snac_embed(const int32_t* frames, int n_frames, int B,
                              const float* const* codebooks, const float* const* proj_w,
-                             const float* const* proj_b, float* z, hipStream_t st);
+                             const float* const* proj_b, float* z, hipStream_t st,
+                             const SnacIO* io = nullptr);
 hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* b,
                          const float* alpha_in, const float* alpha_out, int B, int C, int T,
                          int dil, hipStream_t st);
 hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st);
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
-                           int lo, int hi, float* audio, int16_t* pcm, hipStream_t st);
+                           int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
+                           const SnacIO* io = nullptr);
 hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, const uint64_t* seeds, int64_t per,
-                        hipStream_t st);
+                        hipStream_t st, const SnacIO* io = nullptr);
 
 }  // namespace mx

@@ -32,7 +32,9 @@ struct EmbedPtrs {
 };
 
 __global__ __launch_bounds__(256) void snac_embed_kernel(const int32_t* frames, int n_frames,
-                                                         EmbedPtrs p, float* z) {
+                                                         EmbedPtrs p, float* z,
+                                                         const SnacIO* io) {
+  if (io) frames = io->frames;
   const int t = blockIdx.x, bt = blockIdx.y;
   const int T = 4 * n_frames;
   const int32_t* fr = frames + (size_t)bt * 7 * n_frames;
@@ -294,7 +296,12 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void snac_out_kernel(const float* xs, const float* w,
                                                        const float* b, int T, int lo, int hi,
-                                                       float* audio, int16_t* pcm) {
+                                                       float* audio, int16_t* pcm,
+                                                       const SnacIO* io) {
+  if (io) {
+    audio = io->audio;
+    pcm = io->pcm;
+  }
   const int bt = blockIdx.y;
   const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
   const int part = threadIdx.x & 3;  // channels part*16 .. part*16+15
@@ -335,7 +342,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 // b = i / per draws element j = i % per from seeds[b], so a window's noise depends only on
 // its own seed (batching-invariant streams).
 __global__ void gauss_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* seeds,
-                             int64_t per) {
+                             int64_t per, const SnacIO* io) {
+  if (io) {
+    seed = io->seed;
+    seeds = io->seeds;
+  }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t j = seeds ? (uint64_t)(i % per) : (uint64_t)i;
@@ -346,9 +357,17 @@ __global__ void gauss_kernel(float* out, int64_t n, uint64_t seed, const uint64_
 }
 
 // ---------------------------------------------------------------------------------
+__global__ void set_io_kernel(SnacIO* dst, SnacIO v) { *dst = v; }
+
+hipError_t launch_set_io(SnacIO* dst, const SnacIO& v, hipStream_t st) {
+  hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(1), 0, st, dst, v);
+  return hipGetLastError();
+}
+
 hipError_t launch_snac_embed(const int32_t* frames, int n_frames, int B,
                              const float* const* codebooks, const float* const* proj_w,
-                             const float* const* proj_b, float* z, hipStream_t st) {
+                             const float* const* proj_b, float* z, hipStream_t st,
+                             const SnacIO* io) {
   EmbedPtrs p;
   for (int i = 0; i < 3; ++i) {
     p.cb[i] = codebooks[i];
@@ -356,7 +375,7 @@ hipError_t launch_snac_embed(const int32_t* frames, int n_frames, int B,
     p.b[i] = proj_b[i];
   }
   hipLaunchKernelGGL(snac_embed_kernel, dim3(4 * n_frames, B), dim3(256), 0, st, frames,
-                     n_frames, p, z);
+                     n_frames, p, z, io);
   return hipGetLastError();
 }
 
@@ -389,16 +408,17 @@ hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
 }
 
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
-                           int lo, int hi, float* audio, int16_t* pcm, hipStream_t st) {
+                           int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
+                           const SnacIO* io) {
   hipLaunchKernelGGL(snac_out_kernel, dim3((T + 63) / 64, B), dim3(256), 0, st, xs, w, b, T, lo,
-                     hi, audio, pcm);
+                     hi, audio, pcm, io);
   return hipGetLastError();
 }
 
 hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, const uint64_t* seeds, int64_t per,
-                        hipStream_t st) {
+                        hipStream_t st, const SnacIO* io) {
   hipLaunchKernelGGL(gauss_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n,
-                     seed, seeds, per);
+                     seed, seeds, per, io);
   return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@ VARIANTS = {
     "rpw_gu4": {"rpw_gu": 4},
     "rpw_down2": {"rpw_down": 2},
     "wpb8": {"gemv_wpb": 8},
+    "gu4_down2": {"rpw_gu": 4, "rpw_down": 2},
 }
 
 
