@@ -1059,6 +1059,7 @@ struct mx_snac {
   size_t buf_elems = 0;
   bool final = false;
   SnacIO* io = nullptr;  // device copy of the per-call pointers read by captured windows
+  hipStream_t cap = nullptr;  // capture stream (the caller's may be the null stream)
   std::map<std::array<int, 4>, hipGraphExec_t> graphs;  // (n_frames, batch, lo, hi)
   std::vector<hipGraph_t> graph_defs;
 };
@@ -1299,10 +1300,11 @@ extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, i
   auto it = s->graphs.find(key);
   if (it == s->graphs.end()) {
     hipGraph_t g = nullptr;
-    MX_TRY(s, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    if (!s->cap) MX_TRY(s, hipStreamCreateWithFlags(&s->cap, hipStreamNonBlocking));
+    MX_TRY(s, hipStreamBeginCapture(s->cap, hipStreamCaptureModeRelaxed));
     const int rc = snac_enqueue(s, nullptr, n_frames, batch, nullptr, 0, nullptr, nullptr,
-                                nullptr, lo, hi, st, s->io);
-    hipError_t e2 = hipStreamEndCapture(st, &g);
+                                nullptr, lo, hi, s->cap, s->io);
+    hipError_t e2 = hipStreamEndCapture(s->cap, &g);
     if (rc != MX_OK) {
       if (g) (void)hipGraphDestroy(g);
       return rc;
@@ -1329,6 +1331,7 @@ extern "C" void mx_snac_destroy(mx_snac* s) {
   (void)hipSetDevice(s->device);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto g : s->graph_defs) (void)hipGraphDestroy(g);
+  if (s->cap) (void)hipStreamDestroy(s->cap);
   for (void* p : s->allocs) (void)hipFree(p);
   delete s;
 }
