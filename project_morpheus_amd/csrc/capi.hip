@@ -1054,6 +1054,8 @@ struct mx_snac {
   std::map<std::string, int64_t> expect;
   std::vector<void*> allocs;
   float* up_packed[4][8] = {};  // per block, per phase: [Cout][2*Cin]
+  std::map<std::string, uint16_t*> wbf;  // conv-GEMM weights as bf16 planes [3][M][K]
+  uint16_t* up_bf[4][8] = {};
   int up_delta[4][8][2] = {};
   float *bufA = nullptr, *bufB = nullptr, *bufC = nullptr, *noise = nullptr;
   size_t buf_elems = 0;
@@ -1183,6 +1185,34 @@ extern "C" int mx_snac_finalize(mx_snac* s) {
       s->up_delta[b][ph][1] = q - 1;
     }
   }
+  // the conv-GEMM operands: every dense weight as three bf16 planes
+  auto planes = [&](const float* src, int64_t n, uint16_t** dst) -> int {
+    if (!*dst) {
+      void* p = nullptr;
+      MX_TRY(s, hipMalloc(&p, (size_t)n * 3 * 2));
+      s->allocs.push_back(p);
+      *dst = (uint16_t*)p;
+    }
+    MX_TRY(s, launch_split_planes(src, *dst, n, nullptr));
+    return MX_OK;
+  };
+  std::vector<std::string> dense{"in.pw.w"};
+  for (int b = 0; b < 4; ++b) {
+    const std::string p = "b" + std::to_string(b) + ".";
+    dense.push_back(p + "noise.w");
+    for (int r = 0; r < 3; ++r) dense.push_back(p + "r" + std::to_string(r) + ".pw.w");
+    const int cin = 1024 >> b, cout = cin / 2;
+    for (int ph = 0; ph < kRates[b]; ++ph) {
+      const int rc = planes(s->up_packed[b][ph], (int64_t)cout * 2 * cin, &s->up_bf[b][ph]);
+      if (rc != MX_OK) return rc;
+    }
+  }
+  for (const auto& n : dense) {
+    uint16_t*& d = s->wbf[n];
+    const int rc = planes(s->w[n], s->expect[n], &d);
+    if (rc != MX_OK) return rc;
+  }
+  MX_TRY(s, hipDeviceSynchronize());
   s->final = true;
   return MX_OK;
 }
@@ -1204,6 +1234,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
                         const float* noise, uint64_t seed, const uint64_t* seeds, int16_t* pcm,
                         float* audio, int lo, int hi, hipStream_t st, const SnacIO* io) {
   auto W = [&](const std::string& n) { return s->w[n]; };
+  auto WB = [&](const std::string& n) -> const uint16_t* { return s->wbf.at(n); };
   const int B = batch;
   int T = 4 * n_frames;
   float* A = s->bufA;  // block activations x
@@ -1223,7 +1254,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
   MX_TRY(s, launch_dwconv(A, Bf, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
   {
     ConvGemmArgs g{};
-    g.Aph[0] = W("in.pw.w"); g.X = Bf; g.bias = W("in.pw.b"); g.out = A; g.M = 1024; g.Cin = 768;
+    g.Abf[0] = WB("in.pw.w"); g.X = Bf; g.bias = W("in.pw.b"); g.out = A; g.M = 1024; g.Cin = 768;
     g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1; g.col_stride = 1; g.epi = CG_STORE;
     g.out2 = Cs; g.alpha2 = W("b0.alpha");
     pick_tiles(g, 1);
@@ -1237,7 +1268,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
     {  // ConvTranspose1d on Snake(x): all sr phases in one launch, Cs [cin][T] -> Bf [cout][To]
       ConvGemmArgs g{};
       for (int ph = 0; ph < sr; ++ph) {
-        g.Aph[ph] = s->up_packed[b][ph];
+        g.Abf[ph] = s->up_bf[b][ph];
         g.dph[ph][0] = s->up_delta[b][ph][0];
         g.dph[ph][1] = s->up_delta[b][ph][1];
       }
@@ -1249,7 +1280,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
     T = To;
     {  // NoiseBlock: A = Bf + noise * (Wn Bf)
       ConvGemmArgs g{};
-      g.Aph[0] = W(p + "noise.w"); g.X = Bf; g.R = Bf; g.noise = nz + noff; g.noise_stride = nlen;
+      g.Abf[0] = WB(p + "noise.w"); g.X = Bf; g.R = Bf; g.noise = nz + noff; g.noise_stride = nlen;
       g.out = A; g.M = cout; g.Cin = cout; g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1;
       g.col_stride = 1; g.epi = CG_NOISE;
       pick_tiles(g, 1);
@@ -1261,7 +1292,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
       MX_TRY(s, launch_dwconv(A, Bf, W(q + "dw.w"), W(q + "dw.b"), W(q + "alpha1"),
                               W(q + "alpha2"), B, cout, T, kDil[r], st));
       ConvGemmArgs g{};
-      g.Aph[0] = W(q + "pw.w"); g.X = Bf; g.bias = W(q + "pw.b"); g.R = A; g.out = A;
+      g.Abf[0] = WB(q + "pw.w"); g.X = Bf; g.bias = W(q + "pw.b"); g.R = A; g.out = A;
       g.M = cout; g.Cin = cout; g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1; g.col_stride = 1;
       g.epi = CG_RESID;
       if (r == 2) {  // the block's output feeds Snake -> next ConvTranspose / output conv

@@ -9,7 +9,7 @@ namespace mx {
 enum { CG_STORE = 0, CG_RESID = 1, CG_NOISE = 2 };
 
 struct ConvGemmArgs {
-  const float* Aph[8];  // per phase: [M][nseg*Cin] row-major (ConvTranspose packed per phase)
+  const uint16_t* Abf[8];  // per phase: bf16 planes [3][M][nseg*Cin] (ConvTranspose packed per phase)
   int dph[8][2];        // per phase: time shift of each K segment
   const float* X;       // [B][Cin][Tin]
   const float* bias;    // [M] or null
@@ -46,6 +46,7 @@ hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* 
                          const float* alpha_in, const float* alpha_out, int B, int C, int T,
                          int dil, hipStream_t st);
 hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st);
+hipError_t launch_split_planes(const float* src, uint16_t* dst, int64_t n, hipStream_t st);
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
                            int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
                            const SnacIO* io = nullptr);

@@ -1,18 +1,18 @@
-// SNAC 24 kHz codec decoder on MI355X (gfx950), fp32 end to end.
+// SNAC 24 kHz codec decoder on MI355X (gfx950), fp32 arithmetic.
 //
 // Replaces snac.SNAC.decode (third-party snac 1.2.x; call site
 // Morpheus_Client/tts_engine/speechpipe.py:118) plus the slice / PCM16 epilogue
 // (speechpipe.py:122-129).  Every dense contraction (1x1 convs, NoiseBlock linear,
-// polyphase ConvTranspose1d) runs as one "segmented conv-GEMM" on the exact-f32 MFMA
-// (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain), with the Snake
-// activation fused into the B-operand loader and bias / residual / noise fused into the
-// epilogue.  Depthwise dilated k7 convs stage a haloed, Snake-activated tile in LDS.
+// polyphase ConvTranspose1d) runs as one "segmented conv-GEMM" on the bf16 MFMA with both
+// fp32 operands split into three bf16 parts (fp32-accurate products), the Snake activation
+// of the next consumer and bias / residual / noise fused into the epilogue.  Depthwise
+// dilated k7 convs stage a haloed, Snake-activated tile in LDS.
 #include "mx_common.h"
 #include "mx_snac_kernels.h"
+#include "mx_rows_common.h"
 
 namespace mx {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float snake(float x, float a) {
   // layers.py snake(): x + (alpha + 1e-9).reciprocal() * sin(alpha * x)^2
@@ -103,16 +103,92 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, c
 }
 
 // ---------------------------------------------------------------------------------
-// Segmented conv-GEMM on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32), operands straight
-// from global memory (weights are read once per column tile, activations are L2-resident).
+// Segmented conv-GEMM on the bf16 MFMA (v_mfma_f32_16x16x32_bf16) with fp32 operands split
+// into three bf16 parts each (x = x0 + x1 + x2, w = w0 + w1 + w2, exact to fp32 rounding).
+// The six products whose part indices sum to <= 2 are kept; the dropped ones are below
+// 2^-24 relative, i.e. fp32 rounding.  Six 16x16x32 MFMAs (96 cycles) replace
+// eight 16x16x4 f32 MFMAs (256 cycles) per 32-deep k step of a 16x16 tile.
 //   out[b][m][col_stride*n + ph] = epi( sum_seg sum_ci A_ph[m][seg*Cin+ci] X[b][ci][n+d_ph,seg] )
+// Weights are pre-split at finalize into three bf16 planes [3][M][nseg*Cin]; a lane's A
+// fragment (row c, k = 8g..8g+7) is one 16-byte load per plane.  The B fragment (column n,
+// the same 8 k) is gathered from X [ci][t] and split in registers.
 // One block = one 32 x (16*NSUB) output tile of one (phase, window); its WK waves split K
 // and their partial tiles are summed in LDS in a fixed order (deterministic, no atomics).
-// MFMA j of a 16-deep k chunk contracts k = kc + 4g + j over the lane groups g, so every
-// lane fetches its A operand as one float4 (4 consecutive k of one row).
 // Grid (ceil(Tin / (16*NSUB)), M / 32, nphase * B).
 // ---------------------------------------------------------------------------------
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using rows::bf16x8;
+using rows::f32x4;
+
+template <int NSUB>
+__device__ __forceinline__ void conv_gemm_tile(const ConvGemmArgs& a, int k_begin, int k_end,
+                                               int n0, int m0, int ph, int bt, int lane,
+                                               f32x4 (&acc)[2][NSUB]) {
+  const int c = lane & 15, g = lane >> 4;
+  const uint16_t* A = a.Abf[ph];
+  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
+  const int Ktot = a.nseg * a.Cin;
+  const size_t plane = (size_t)a.M * Ktot;
+  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tn[NSUB];
+  bool nok[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) {
+    tn[j] = n0 + 16 * j + c;
+    nok[j] = tn[j] < a.Tin;
+  }
+  const uint16_t* Ar0 = A + (size_t)(m0 + c) * Ktot + 8 * g;
+  const uint16_t* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot + 8 * g;
+  for (int kc = k_begin; kc < k_end; kc += 32) {
+    bf16x8 af[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      af[0][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ar0 + p * plane + kc));
+      af[1][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ar1 + p * plane + kc));
+    }
+    const int seg = kc >= a.Cin ? 1 : 0;  // a 32-chunk never straddles segments (Cin % 32 == 0)
+    const int ci0 = kc + 8 * g - seg * a.Cin;
+    const int d = seg ? d1 : d0;
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const int t = tn[j] + d;
+      const bool ok = nok[j] && t >= 0 && t < a.Tin;
+      const int tc = min(max(t, 0), a.Tin - 1);
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
+        x[e] = ok ? v : 0.f;
+      }
+      bf16x8 xf[3];
+      rows::split_parts<3>(x, xf);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // smallest terms first
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], xf[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], xf[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], xf[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[0], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void conv_gemm_store(const ConvGemmArgs& a, float v, int m, int n,
+                                                int ph, int bt) {
+  const int col = a.col_stride * n + ph;
+  if (a.bias) v += a.bias[m];
+  const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
+  if (a.epi == CG_RESID) v = a.R[o] + v;
+  else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
+  a.out[o] = v;
+  if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
+}
 
 template <int WK, int NSUB>
 __global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
@@ -121,97 +197,30 @@ __global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
   const int c = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int ph = blockIdx.z / a.B, bt = blockIdx.z - ph * a.B;
-  const float* A = a.Aph[ph];
-  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
-  const int Ktot = a.nseg * a.Cin;
-  const int Kw = Ktot / WK;
-  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
-
+  const int Kw = a.nseg * a.Cin / WK;
   f32x4 acc[2][NSUB];
+  conv_gemm_tile<NSUB>(a, wk * Kw, (wk + 1) * Kw, n0, m0, ph, bt, lane, acc);
+  // deterministic cross-wave K reduction through LDS: tile [BM][BN] per wave
+  __shared__ float red[WK][BM * BN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < NSUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // this lane's output columns (B operand) and their validity
-  int tn[NSUB];
-  bool nok[NSUB];
+    for (int j = 0; j < NSUB; ++j)
 #pragma unroll
-  for (int j = 0; j < NSUB; ++j) {
-    tn[j] = n0 + 16 * j + c;
-    nok[j] = tn[j] < a.Tin;
-  }
-  const float* Ar0 = A + (size_t)(m0 + c) * Ktot;
-  const float* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot;
-  for (int kc = wk * Kw; kc < (wk + 1) * Kw; kc += 16) {
-    const int k4 = kc + 4 * g;
-    const float4 a0 = *reinterpret_cast<const float4*>(Ar0 + k4);
-    const float4 a1 = *reinterpret_cast<const float4*>(Ar1 + k4);
-    const int seg = kc >= a.Cin ? 1 : 0;  // a 16-chunk never straddles segments
-    const int ci0 = k4 - seg * a.Cin;
-    const int d = seg ? d1 : d0;
-    float bv[NSUB][4];
-#pragma unroll
-    for (int j = 0; j < NSUB; ++j) {
-      const int t = tn[j] + d;
-      const bool ok = nok[j] && t >= 0 && t < a.Tin;
-      const int tc = min(max(t, 0), a.Tin - 1);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
-        bv[j][e] = ok ? v : 0.f;
-      }
-    }
-    const float av0[4] = {a0.x, a0.y, a0.z, a0.w};
-    const float av1[4] = {a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-#pragma unroll
-      for (int j = 0; j < NSUB; ++j) {
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv[j][e], acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv[j][e], acc[1][j], 0, 0, 0);
-      }
-    }
-  }
-
-  // deterministic cross-wave K reduction through LDS: tile [BM][BN] per wave
-  __shared__ float red[WK][BM * BN];
-  if (WK > 1) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NSUB; ++j)
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg)
-          red[wk][(16 * i + 4 * g + rg) * BN + 16 * j + c] = acc[i][j][rg];
-    __syncthreads();
-  }
-  // epilogue: thread -> tile elements
+      for (int rg = 0; rg < 4; ++rg) red[wk][(16 * i + 4 * g + rg) * BN + 16 * j + c] = acc[i][j][rg];
+  __syncthreads();
   for (int e = threadIdx.x; e < BM * BN; e += WK * 64) {
     const int mm = e / BN, nn = e - mm * BN;
     const int n = n0 + nn;
     if (n >= a.Tin) continue;
-    float v;
-    if (WK > 1) {
-      v = red[0][e];
+    float v = red[0][e];
 #pragma unroll
-      for (int w = 1; w < WK; ++w) v += red[w][e];
-    } else {
-      // WK == 1: the wave's own registers hold the tile; route through LDS anyway
-      v = 0.f;
-    }
-    const int m = m0 + mm;
-    const int col = a.col_stride * n + ph;
-    if (a.bias) v += a.bias[m];
-    const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
-    if (a.epi == CG_RESID) v = a.R[o] + v;
-    else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
-    a.out[o] = v;
-    if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
+    for (int w = 1; w < WK; ++w) v += red[w][e];
+    conv_gemm_store(a, v, m0 + mm, n, ph, bt);
   }
 }
 
-// WK == 1 specialisation of the epilogue path: write straight from registers.
+// WK == 1: one wave per tile, the epilogue straight from registers.
 template <int NSUB>
 __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
   constexpr int BM = 32, BN = 16 * NSUB;
@@ -219,73 +228,36 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
   const int c = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int ph = blockIdx.z / a.B, bt = blockIdx.z - ph * a.B;
-  const float* A = a.Aph[ph];
-  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
-  const int Ktot = a.nseg * a.Cin;
-  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
   f32x4 acc[2][NSUB];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < NSUB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int tn[NSUB];
-  bool nok[NSUB];
-#pragma unroll
-  for (int j = 0; j < NSUB; ++j) {
-    tn[j] = n0 + 16 * j + c;
-    nok[j] = tn[j] < a.Tin;
-  }
-  const float* Ar0 = A + (size_t)(m0 + c) * Ktot;
-  const float* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot;
-  for (int kc = 0; kc < Ktot; kc += 16) {
-    const int k4 = kc + 4 * g;
-    const float4 a0 = *reinterpret_cast<const float4*>(Ar0 + k4);
-    const float4 a1 = *reinterpret_cast<const float4*>(Ar1 + k4);
-    const int seg = kc >= a.Cin ? 1 : 0;
-    const int ci0 = k4 - seg * a.Cin;
-    const int d = seg ? d1 : d0;
-    float bv[NSUB][4];
-#pragma unroll
-    for (int j = 0; j < NSUB; ++j) {
-      const int t = tn[j] + d;
-      const bool ok = nok[j] && t >= 0 && t < a.Tin;
-      const int tc = min(max(t, 0), a.Tin - 1);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
-        bv[j][e] = ok ? v : 0.f;
-      }
-    }
-    const float av0[4] = {a0.x, a0.y, a0.z, a0.w};
-    const float av1[4] = {a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-#pragma unroll
-      for (int j = 0; j < NSUB; ++j) {
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv[j][e], acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv[j][e], acc[1][j], 0, 0, 0);
-      }
-    }
-  }
+  conv_gemm_tile<NSUB>(a, 0, a.nseg * a.Cin, n0, m0, ph, bt, lane, acc);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NSUB; ++j) {
       const int n = n0 + 16 * j + c;
       if (n >= a.Tin) continue;
-      const int col = a.col_stride * n + ph;
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int m = m0 + 16 * i + 4 * g + rg;
-        float v = acc[i][j][rg];
-        if (a.bias) v += a.bias[m];
-        const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
-        if (a.epi == CG_RESID) v = a.R[o] + v;
-        else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
-        a.out[o] = v;
-        if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
-      }
+      for (int rg = 0; rg < 4; ++rg) conv_gemm_store(a, acc[i][j][rg], m0 + 16 * i + 4 * g + rg, n, ph, bt);
     }
+}
+
+// fp32 [n] -> three bf16 planes [3][n] (x = p0 + p1 + p2), for the conv-GEMM weights.
+__global__ void split_planes_kernel(const float* src, uint16_t* dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float r = src[i];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const uint32_t pk = pack2_bf16(r, 0.f);
+    dst[p * n + i] = (uint16_t)(pk & 0xffffu);
+    r -= bf16_lo(pk);
+  }
+}
+
+hipError_t launch_split_planes(const float* src, uint16_t* dst, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src,
+                     dst, n);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -390,7 +362,7 @@ hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* 
 
 hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
   const int Ktot = a.nseg * a.Cin;
-  if (a.M % 32 || a.Cin % 16 || Ktot % (16 * a.wk)) return hipErrorInvalidValue;
+  if (a.M % 32 || a.Cin % 32 || Ktot % (32 * a.wk)) return hipErrorInvalidValue;
   const int bn = 16 * a.nsub;
   const dim3 grid((a.Tin + bn - 1) / bn, a.M / 32, nphase * a.B);
 #define MX_CG(WK_, NS_)                                                                   \
