@@ -1250,7 +1250,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
   const float* cb[3] = {W("q0.codebook"), W("q1.codebook"), W("q2.codebook")};
   const float* pw[3] = {W("q0.out_proj.w"), W("q1.out_proj.w"), W("q2.out_proj.w")};
   const float* pb[3] = {W("q0.out_proj.b"), W("q1.out_proj.b"), W("q2.out_proj.b")};
-  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, A, st, io));    // A: [768][T]
+  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, A, st, io));    // A: [T][768]
   MX_TRY(s, launch_dwconv(A, Bf, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
   {
     ConvGemmArgs g{};
@@ -1258,14 +1258,14 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
     g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1; g.col_stride = 1; g.epi = CG_STORE;
     g.out2 = Cs; g.alpha2 = W("b0.alpha");
     pick_tiles(g, 1);
-    MX_TRY(s, launch_conv_gemm(g, 1, st));                                      // A: [1024][T]
+    MX_TRY(s, launch_conv_gemm(g, 1, st));                                      // A: [T][1024]
   }
   int noff = 0;
   for (int b = 0; b < 4; ++b) {
     const int cin = 1024 >> b, cout = cin / 2, sr = kRates[b];
     const std::string p = "b" + std::to_string(b) + ".";
     const int To = T * sr;
-    {  // ConvTranspose1d on Snake(x): all sr phases in one launch, Cs [cin][T] -> Bf [cout][To]
+    {  // ConvTranspose1d on Snake(x): all sr phases in one launch, Cs [T][cin] -> Bf [To][cout]
       ConvGemmArgs g{};
       for (int ph = 0; ph < sr; ++ph) {
         g.Abf[ph] = s->up_bf[b][ph];

@@ -1,5 +1,5 @@
-// SNAC 24 kHz decoder kernels (snac_kernels.hip).  All fp32 (the reference never casts
-// SNAC: speechpipe.py:43-49), activations laid out [batch][channels][time].
+// SNAC 24 kHz decoder kernels (snac_kernels.hip).  fp32 arithmetic (the reference never casts
+// SNAC: speechpipe.py:43-49), activations channels-last [batch][time][channels].
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -11,13 +11,13 @@ enum { CG_STORE = 0, CG_RESID = 1, CG_NOISE = 2 };
 struct ConvGemmArgs {
   const uint16_t* Abf[8];  // per phase: bf16 planes [3][M][nseg*Cin] (ConvTranspose packed per phase)
   int dph[8][2];        // per phase: time shift of each K segment
-  const float* X;       // [B][Cin][Tin]
+  const float* X;       // [B][Tin][Cin]
   const float* bias;    // [M] or null
-  const float* R;       // residual source [B][M][Tout] (CG_RESID / CG_NOISE)
+  const float* R;       // residual source [B][Tout][M] (CG_RESID / CG_NOISE)
   const float* noise;   // window b's noise at noise + b * noise_stride (CG_NOISE)
   int noise_stride;
-  float* out;           // [B][M][Tout]
-  float* out2;          // optional: Snake(out, alpha2) [B][M][Tout] for the next consumer
+  float* out;           // [B][Tout][M]
+  float* out2;          // optional: Snake(out, alpha2) [B][Tout][M] for the next consumer
   const float* alpha2;
   int M, Cin, Tin, Tout, B;
   int nseg;

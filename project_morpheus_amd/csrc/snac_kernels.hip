@@ -23,7 +23,7 @@ __device__ __forceinline__ float snake(float x, float a) {
 // ---------------------------------------------------------------------------------
 // RVQ from_codes (vq.py): z[c][t] = sum_i out_proj_i(codebook_i[code_i[t / stride_i]])
 // frames: [B][7N] codes in speechpipe order; de-interleave per speechpipe.py:84-98.
-// Grid (4N, B), block 256.
+// z is channels-last [B][4N][768].  Grid (4N, B), block 256.
 // ---------------------------------------------------------------------------------
 struct EmbedPtrs {
   const float* cb[3];
@@ -66,40 +66,51 @@ __global__ __launch_bounds__(256) void snac_embed_kernel(const int32_t* frames, 
       for (int k = 0; k < 8; ++k) v = fmaf(p.w[i][c * 8 + k], e[i][k], v);
       zc += v;
     }
-    z[((size_t)bt * 768 + c) * T + t] = zc;
+    z[((size_t)bt * T + t) * 768 + c] = zc;
   }
 }
 
 // ---------------------------------------------------------------------------------
-// Depthwise k7 dilated conv, "same" padding 3*dil, optional Snake on input and output.
-// Grid (ceil(T/256), C, B), block 256; haloed Snake(x) tile in LDS.
+// Depthwise k7 dilated conv, "same" padding 3*dil, optional Snake on input and output, on
+// channels-last activations [B][T][C] (every SNAC activation is channels-last, so a conv-GEMM
+// B fragment -- 8 consecutive channels at one time step -- is two 16-byte loads).
+// Block = 64 channels x 4 time rows; the 64-step output tile reads a haloed Snake(x) tile
+// staged once in LDS (Snake evaluated once per input).  Grid (ceil(T/64), C/64, B).
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, const float* w,
                                                      const float* b, const float* ain,
                                                      const float* aout, int C, int T, int dil) {
-  const int c = blockIdx.y, bt = blockIdx.z;
-  const int t0 = blockIdx.x * 256;
+  constexpr int TT = 64;
+  const int cl = threadIdx.x & 63, tr = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl, t0 = blockIdx.x * TT, bt = blockIdx.z;
   const int halo = 3 * dil;
-  __shared__ float tile[256 + 2 * 27];
-  const float* xr = x + ((size_t)bt * C + c) * T;
+  __shared__ float tile[TT + 54][64];
+  const float* xb = x + (size_t)bt * T * C + c;
   const float a_in = ain ? ain[c] : 0.f;
-  for (int i = threadIdx.x; i < 256 + 2 * halo; i += 256) {
+  for (int i = tr; i < TT + 2 * halo; i += 4) {
     const int t = t0 - halo + i;
     float v = 0.f;
     if (t >= 0 && t < T) {
-      v = xr[t];
+      v = xb[(size_t)t * C];
       if (ain) v = snake(v, a_in);
     }
-    tile[i] = v;
+    tile[i][cl] = v;
   }
   __syncthreads();
-  const int t = t0 + threadIdx.x;
-  if (t >= T) return;
-  float acc = b[c];
+  float wk[7];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) acc = fmaf(w[c * 7 + k], tile[threadIdx.x + k * dil], acc);
-  if (aout) acc = snake(acc, aout[c]);
-  y[((size_t)bt * C + c) * T + t] = acc;
+  for (int k = 0; k < 7; ++k) wk[k] = w[c * 7 + k];
+  const float bias = b[c], a_out = aout ? aout[c] : 0.f;
+  float* yb = y + (size_t)bt * T * C + c;
+  for (int i = tr; i < TT; i += 4) {
+    const int t = t0 + i;
+    if (t >= T) break;
+    float acc = bias;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc = fmaf(wk[k], tile[i + k * dil][cl], acc);
+    if (aout) acc = snake(acc, a_out);
+    yb[(size_t)t * C] = acc;
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -108,10 +119,10 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, c
 // The six products whose part indices sum to <= 2 are kept; the dropped ones are below
 // 2^-24 relative, i.e. fp32 rounding.  Six 16x16x32 MFMAs (96 cycles) replace
 // eight 16x16x4 f32 MFMAs (256 cycles) per 32-deep k step of a 16x16 tile.
-//   out[b][m][col_stride*n + ph] = epi( sum_seg sum_ci A_ph[m][seg*Cin+ci] X[b][ci][n+d_ph,seg] )
+//   out[b][col_stride*n + ph][m] = epi( sum_seg sum_ci A_ph[m][seg*Cin+ci] X[b][n+d_ph,seg][ci] )
 // Weights are pre-split at finalize into three bf16 planes [3][M][nseg*Cin]; a lane's A
 // fragment (row c, k = 8g..8g+7) is one 16-byte load per plane.  The B fragment (column n,
-// the same 8 k) is gathered from X [ci][t] and split in registers.
+// the same 8 k) is two 16-byte loads from channels-last X [t][ci], split in registers.
 // One block = one 32 x (16*NSUB) output tile of one (phase, window); its WK waves split K
 // and their partial tiles are summed in LDS in a fixed order (deterministic, no atomics).
 // Grid (ceil(Tin / (16*NSUB)), M / 32, nphase * B).
@@ -128,7 +139,7 @@ __device__ __forceinline__ void conv_gemm_tile(const ConvGemmArgs& a, int k_begi
   const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
   const int Ktot = a.nseg * a.Cin;
   const size_t plane = (size_t)a.M * Ktot;
-  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;
+  const float* X = a.X + (size_t)bt * a.Cin * a.Tin;  // [Tin][Cin]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -157,11 +168,12 @@ __device__ __forceinline__ void conv_gemm_tile(const ConvGemmArgs& a, int k_begi
       const int t = tn[j] + d;
       const bool ok = nok[j] && t >= 0 && t < a.Tin;
       const int tc = min(max(t, 0), a.Tin - 1);
-      float x[8];
+      const float4* xp = reinterpret_cast<const float4*>(X + (size_t)tc * a.Cin + ci0);
+      const float4 lo = xp[0], hi = xp[1];
+      float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      if (!ok) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = X[(size_t)(ci0 + e) * a.Tin + tc];
-        x[e] = ok ? v : 0.f;
+        for (int e = 0; e < 8; ++e) x[e] = 0.f;
       }
       bf16x8 xf[3];
       rows::split_parts<3>(x, xf);
@@ -183,11 +195,32 @@ __device__ __forceinline__ void conv_gemm_store(const ConvGemmArgs& a, float v, 
                                                 int ph, int bt) {
   const int col = a.col_stride * n + ph;
   if (a.bias) v += a.bias[m];
-  const size_t o = ((size_t)bt * a.M + m) * a.Tout + col;
+  const size_t o = ((size_t)bt * a.Tout + col) * a.M + m;
   if (a.epi == CG_RESID) v = a.R[o] + v;
   else if (a.epi == CG_NOISE) v = a.R[o] + a.noise[(size_t)bt * a.noise_stride + col] * v;
   a.out[o] = v;
   if (a.out2) a.out2[o] = snake(v, a.alpha2[m]);
+}
+
+// 4 consecutive channels m .. m+3 of one column: 16-byte accesses in the channels-last layout
+__device__ __forceinline__ void conv_gemm_store4(const ConvGemmArgs& a, f32x4 v, int m, int n,
+                                                 int ph, int bt) {
+  const int col = a.col_stride * n + ph;
+  if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + m);
+  const size_t o = ((size_t)bt * a.Tout + col) * a.M + m;
+  if (a.epi == CG_RESID) {
+    v += *reinterpret_cast<const f32x4*>(a.R + o);
+  } else if (a.epi == CG_NOISE) {
+    const float nz = a.noise[(size_t)bt * a.noise_stride + col];
+    v = *reinterpret_cast<const f32x4*>(a.R + o) + nz * v;
+  }
+  *reinterpret_cast<f32x4*>(a.out + o) = v;
+  if (a.out2) {
+    f32x4 s2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s2[r] = snake(v[r], a.alpha2[m + r]);
+    *reinterpret_cast<f32x4*>(a.out2 + o) = s2;
+  }
 }
 
 template <int WK, int NSUB>
@@ -210,12 +243,13 @@ __global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
       for (int rg = 0; rg < 4; ++rg) red[wk][(16 * i + 4 * g + rg) * BN + 16 * j + c] = acc[i][j][rg];
   __syncthreads();
   for (int e = threadIdx.x; e < BM * BN; e += WK * 64) {
-    const int mm = e / BN, nn = e - mm * BN;
+    const int nn = e / BM, mm = e - nn * BM;  // consecutive threads: consecutive channels
     const int n = n0 + nn;
     if (n >= a.Tin) continue;
-    float v = red[0][e];
+    const int ei = mm * BN + nn;
+    float v = red[0][ei];
 #pragma unroll
-    for (int w = 1; w < WK; ++w) v += red[w][e];
+    for (int w = 1; w < WK; ++w) v += red[w][ei];
     conv_gemm_store(a, v, m0 + mm, n, ph, bt);
   }
 }
@@ -236,8 +270,7 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
     for (int j = 0; j < NSUB; ++j) {
       const int n = n0 + 16 * j + c;
       if (n >= a.Tin) continue;
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) conv_gemm_store(a, acc[i][j][rg], m0 + 16 * i + 4 * g + rg, n, ph, bt);
+      conv_gemm_store4(a, acc[i][j], m0 + 16 * i + 4 * g, n, ph, bt);
     }
 }
 
@@ -277,17 +310,22 @@ __global__ __launch_bounds__(256) void snac_out_kernel(const float* xs, const fl
   const int bt = blockIdx.y;
   const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
   const int part = threadIdx.x & 3;  // channels part*16 .. part*16+15
-  const float* xb = xs + (size_t)bt * 64 * T;
+  const float* xb = xs + (size_t)bt * T * 64 + part * 16;  // channels-last [T][64]
   float acc = 0.f;
   if (t < T) {
-    for (int cc = 0; cc < 16; ++cc) {
-      const int ch = part * 16 + cc;
-      const float* xr = xb + (size_t)ch * T;
 #pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        const int tt = t + k - 3;
-        const float v = (tt >= 0 && tt < T) ? xr[tt] : 0.f;
-        acc = fmaf(w[ch * 7 + k], v, acc);
+    for (int k = 0; k < 7; ++k) {
+      const int tt = t + k - 3;
+      if (tt < 0 || tt >= T) continue;
+      const float4* xr = reinterpret_cast<const float4*>(xb + (size_t)tt * 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = xr[q];
+        const int ch = part * 16 + 4 * q;
+        acc = fmaf(w[ch * 7 + k], v.x, acc);
+        acc = fmaf(w[(ch + 1) * 7 + k], v.y, acc);
+        acc = fmaf(w[(ch + 2) * 7 + k], v.z, acc);
+        acc = fmaf(w[(ch + 3) * 7 + k], v.w, acc);
       }
     }
   }
@@ -354,8 +392,8 @@ hipError_t launch_snac_embed(const int32_t* frames, int n_frames, int B,
 hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* b,
                          const float* alpha_in, const float* alpha_out, int B, int C, int T,
                          int dil, hipStream_t st) {
-  if (dil > 9) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dwconv_kernel, dim3((T + 255) / 256, C, B), dim3(256), 0, st, x, y, w, b,
+  if (dil > 9 || C % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dwconv_kernel, dim3((T + 63) / 64, C / 64, B), dim3(256), 0, st, x, y, w, b,
                      alpha_in, alpha_out, C, T, dil);
   return hipGetLastError();
 }
