@@ -1220,12 +1220,25 @@ extern "C" int mx_snac_finalize(mx_snac* s) {
 // Tile choice for one conv-GEMM: 64-wide column tiles on long sequences, and as many
 // K-splitting waves per tile as keep the launch near 2k waves (early stages have few
 // output columns and long K, late stages the opposite).
+// Window batch from which the block-tiled conv-GEMM is used.  Its point is sharing each A
+// (weight) fragment across the windows' columns; one window gains nothing from it and the
+// one-wave kernels give small batches 4-8x the blocks (N7_B1 0.41 vs 0.55 ms, N7_B4 0.18 vs
+// 0.23 ms per window; profiles/r02_snac_tiled_timing.log).
+static int snac_tiled_min_batch() {
+  static const int v = [] {
+    const char* e = getenv("MORPHEUS_MX_SNAC_TILED_MIN_BATCH");
+    return e ? atoi(e) : 8;
+  }();
+  return v;
+}
+
 static void pick_tiles(ConvGemmArgs& g, int nphase) {
+  g.tiled = g.M % 64 == 0 && g.B >= snac_tiled_min_batch();
   g.nsub = g.Tin >= 2048 ? 4 : 2;
   const int tiles = (g.M / 32) * ((g.Tin + 16 * g.nsub - 1) / (16 * g.nsub)) * nphase * g.B;
   const int Ktot = g.nseg * g.Cin;
   g.wk = 1;
-  while (g.wk < 8 && tiles * g.wk * 2 <= 2048 && Ktot % (32 * g.wk) == 0 && Ktot / (2 * g.wk) >= 64)
+  while (g.wk < 8 && tiles * g.wk * 2 <= 2048 && Ktot % (128 * g.wk) == 0 && Ktot / (2 * g.wk) >= 64)
     g.wk *= 2;
 }
 

@@ -24,6 +24,7 @@ struct ConvGemmArgs {
   int col_stride;       // output column = col_stride * n + phase
   int epi;
   int wk, nsub;         // waves splitting K; 16-column subtiles per tile
+  int tiled;            // 1: block-tiled kernel over the windows' concatenated columns
 };
 
 // Per-call I/O of a graph-captured window decode: the captured kernels read these from a

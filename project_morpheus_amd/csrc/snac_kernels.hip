@@ -15,8 +15,12 @@ namespace mx {
 
 
 __device__ __forceinline__ float snake(float x, float a) {
-  // layers.py snake(): x + (alpha + 1e-9).reciprocal() * sin(alpha * x)^2
-  const float s = sinf(a * x);
+  // layers.py snake(): x + (alpha + 1e-9).reciprocal() * sin(alpha * x)^2.  The sine is the
+  // hardware v_sin_f32 (8 cycles) on the fp32 argument reduced to [0, 1) revolutions: the
+  // library sinf (~30 instructions) made the Snake stages VALU-bound.  CPU emulation of this
+  // reduction: audio RMS 6e-7 vs torch.sin (scripts/snac_fastsin_emulation.py).
+  const float rev = (a * x) * 0.15915494309189535f;
+  const float s = __builtin_amdgcn_sinf(rev - floorf(rev));
   return x + (1.0f / (a + 1e-9f)) * (s * s);
 }
 
@@ -74,13 +78,14 @@ __global__ __launch_bounds__(256) void snac_embed_kernel(const int32_t* frames, 
 // Depthwise k7 dilated conv, "same" padding 3*dil, optional Snake on input and output, on
 // channels-last activations [B][T][C] (every SNAC activation is channels-last, so a conv-GEMM
 // B fragment -- 8 consecutive channels at one time step -- is two 16-byte loads).
-// Block = 64 channels x 4 time rows; the 64-step output tile reads a haloed Snake(x) tile
-// staged once in LDS (Snake evaluated once per input).  Grid (ceil(T/64), C/64, B).
+// Block = 64 channels x 4 time rows; the TT-step output tile reads a haloed Snake(x) tile
+// staged once in LDS (Snake evaluated once per input).  Grid (ceil(T/TT), C/64, B): TT = 64
+// for the batched shapes, 16 for single windows (4x the blocks; the halo costs more there).
 // ---------------------------------------------------------------------------------
+template <int TT>
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, const float* w,
                                                      const float* b, const float* ain,
                                                      const float* aout, int C, int T, int dil) {
-  constexpr int TT = 64;
   const int cl = threadIdx.x & 63, tr = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl, t0 = blockIdx.x * TT, bt = blockIdx.z;
   const int halo = 3 * dil;
@@ -153,41 +158,59 @@ __device__ __forceinline__ void conv_gemm_tile(const ConvGemmArgs& a, int k_begi
   }
   const uint16_t* Ar0 = A + (size_t)(m0 + c) * Ktot + 8 * g;
   const uint16_t* Ar1 = A + (size_t)(m0 + 16 + c) * Ktot + 8 * g;
-  for (int kc = k_begin; kc < k_end; kc += 32) {
-    bf16x8 af[2][3];
+  // two-stage pipeline: the next 32-deep step's A planes and X pieces are in flight while
+  // this step splits X and runs its MFMAs (k ranges are multiples of 64: launch_conv_gemm)
+  uint4 ab[2][2][3];
+  float4 xb[2][NSUB][2];
+  auto load = [&](int kc, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      af[0][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ar0 + p * plane + kc));
-      af[1][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Ar1 + p * plane + kc));
+      ab[buf][0][p] = *reinterpret_cast<const uint4*>(Ar0 + p * plane + kc);
+      ab[buf][1][p] = *reinterpret_cast<const uint4*>(Ar1 + p * plane + kc);
     }
     const int seg = kc >= a.Cin ? 1 : 0;  // a 32-chunk never straddles segments (Cin % 32 == 0)
     const int ci0 = kc + 8 * g - seg * a.Cin;
     const int d = seg ? d1 : d0;
 #pragma unroll
     for (int j = 0; j < NSUB; ++j) {
+      const int tc = min(max(tn[j] + d, 0), a.Tin - 1);
+      const float4* xp = reinterpret_cast<const float4*>(X + (size_t)tc * a.Cin + ci0);
+      xb[buf][j][0] = xp[0];
+      xb[buf][j][1] = xp[1];
+    }
+  };
+  auto step = [&](int kc, int buf) __attribute__((always_inline)) {
+    const int d = kc >= a.Cin ? d1 : d0;
+    bf16x8 xf[NSUB][3];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
       const int t = tn[j] + d;
       const bool ok = nok[j] && t >= 0 && t < a.Tin;
-      const int tc = min(max(t, 0), a.Tin - 1);
-      const float4* xp = reinterpret_cast<const float4*>(X + (size_t)tc * a.Cin + ci0);
-      const float4 lo = xp[0], hi = xp[1];
+      const float4 lo = xb[buf][j][0], hi = xb[buf][j][1];
       float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       if (!ok) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) x[e] = 0.f;
       }
-      bf16x8 xf[3];
-      rows::split_parts<3>(x, xf);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        // smallest terms first
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], xf[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], xf[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], xf[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], xf[0], acc[i][j], 0, 0, 0);
-      }
+      rows::split_parts<3>(x, xf[j]);
     }
+    // six products, smallest first; 2 x NSUB independent accumulator chains per product
+    constexpr int PA[6] = {1, 0, 2, 0, 1, 0}, PB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, ab[buf][i][PA[q]]), xf[j][PB[q]], acc[i][j], 0, 0, 0);
+  };
+  load(k_begin, 0);
+  for (int kc = k_begin; kc < k_end; kc += 64) {
+    load(kc + 32, 1);
+    step(kc, 0);
+    if (kc + 64 < k_end) load(kc + 64, 0);
+    step(kc + 32, 1);
   }
 }
 
@@ -272,6 +295,107 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
       if (n >= a.Tin) continue;
       conv_gemm_store4(a, acc[i][j], m0 + 16 * i + 4 * g, n, ph, bt);
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Block-tiled conv-GEMM for batched windows (the serving shapes): the B windows' columns are
+// concatenated (column = window * Tin + t), and a 256-thread block computes a 64 x 128 tile
+// over 2 x 2 waves (32 x 64 each).  Per 32-deep k step the block stages A (64 rows x 3 bf16
+// planes) and X (128 columns x 32 channels, split into 3 bf16 parts) ONCE in LDS in MFMA
+// fragment order, so every operand byte fetched from L2 feeds 4-8x more MFMAs than the
+// one-wave kernels above (whose A / X re-fetches made them vector-memory bound: 50-70 TF/s).
+// The next step's global loads are in flight (registers) while this step's MFMAs run.
+// Grid (ceil(B*Tin / 128), M / 64, nphase).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int wm = w & 1, wn = w >> 1;  // wave position in the 2 x 2 block
+  const int ph = blockIdx.z;
+  const int m0 = blockIdx.y * 64;
+  const int ncol = a.B * a.Tin;
+  const int col0 = blockIdx.x * 128;
+  const uint16_t* A = a.Abf[ph];
+  const int Ktot = a.nseg * a.Cin;
+  const size_t plane = (size_t)a.M * Ktot;
+  const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
+  __shared__ uint4 As[3][4][64];    // [plane][m-tile][lane]: A fragments
+  __shared__ uint4 Bs[3][8][64];    // [part][n-tile][lane]: B fragments
+
+  // staging roles: A — row ar = tid / 4, k quarter aq = tid % 4 (8 k, 16 B per plane);
+  // X — column xn = tid / 2, channel half xh = tid % 2 (16 channels, 4 x float4)
+  const int ar = tid >> 2, aq = tid & 3;
+  const uint16_t* Arow = A + (size_t)(m0 + ar) * Ktot + 8 * aq;
+  const int xn = tid >> 1, xh = tid & 1;
+  const int xcol = col0 + xn;
+  const bool xin = xcol < ncol;
+  const int xbt = xin ? xcol / a.Tin : 0, xt = xin ? xcol - xbt * a.Tin : 0;
+  const float* Xw = a.X + (size_t)xbt * a.Tin * a.Cin;
+  uint4 ra[3];
+  float4 rx[4];
+  auto gload = [&](int kc) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) ra[p] = *reinterpret_cast<const uint4*>(Arow + p * plane + kc);
+    const int seg = kc >= a.Cin ? 1 : 0;
+    const int t = xt + (seg ? d1 : d0);
+    const bool ok = xin && t >= 0 && t < a.Tin;
+    const float4* xp = reinterpret_cast<const float4*>(
+        Xw + (size_t)min(max(t, 0), a.Tin - 1) * a.Cin + (kc - seg * a.Cin) + 16 * xh);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rx[q] = ok ? xp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto lstore = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) As[p][ar >> 4][aq * 16 + (ar & 15)] = ra[p];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // 8 channels = k group g' = 2 xh + h of column xn
+      float x[8] = {rx[2 * h].x, rx[2 * h].y, rx[2 * h].z, rx[2 * h].w,
+                    rx[2 * h + 1].x, rx[2 * h + 1].y, rx[2 * h + 1].z, rx[2 * h + 1].w};
+      bf16x8 xf[3];
+      rows::split_parts<3>(x, xf);
+      const int gg = 2 * xh + h;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) Bs[p][xn >> 4][gg * 16 + (xn & 15)] = __builtin_bit_cast(uint4, xf[p]);
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  for (int kc = 0; kc < Ktot; kc += 32) {
+    __syncthreads();  // the previous step's fragments are consumed
+    lstore();
+    __syncthreads();
+    if (kc + 32 < Ktot) gload(kc + 32);
+    bf16x8 af[2][3], bfr[4][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[i][p] = __builtin_bit_cast(bf16x8, As[p][2 * wm + i][lane]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bfr[j][p] = __builtin_bit_cast(bf16x8, Bs[p][4 * wn + j][lane]);
+    constexpr int PA[6] = {1, 0, 2, 0, 1, 0}, PB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][PA[q]], bfr[j][PB[q]], acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + 64 * wn + 16 * j + c;
+    if (col >= ncol) continue;
+    const int bt = col / a.Tin, t = col - bt * a.Tin;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) conv_gemm_store4(a, acc[i][j], m0 + 32 * wm + 16 * i + 4 * g, t, ph, bt);
+  }
 }
 
 // fp32 [n] -> three bf16 planes [3][n] (x = p0 + p1 + p2), for the conv-GEMM weights.
@@ -393,14 +517,24 @@ hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* 
                          const float* alpha_in, const float* alpha_out, int B, int C, int T,
                          int dil, hipStream_t st) {
   if (dil > 9 || C % 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dwconv_kernel, dim3((T + 63) / 64, C / 64, B), dim3(256), 0, st, x, y, w, b,
-                     alpha_in, alpha_out, C, T, dil);
+  if ((int64_t)B * T >= 65536)
+    hipLaunchKernelGGL(dwconv_kernel<64>, dim3((T + 63) / 64, C / 64, B), dim3(256), 0, st, x, y,
+                       w, b, alpha_in, alpha_out, C, T, dil);
+  else
+    hipLaunchKernelGGL(dwconv_kernel<16>, dim3((T + 15) / 16, C / 64, B), dim3(256), 0, st, x, y,
+                       w, b, alpha_in, alpha_out, C, T, dil);
   return hipGetLastError();
 }
 
 hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
   const int Ktot = a.nseg * a.Cin;
-  if (a.M % 32 || a.Cin % 32 || Ktot % (32 * a.wk)) return hipErrorInvalidValue;
+  if (a.tiled) {
+    if (a.M % 64 || a.Cin % 32) return hipErrorInvalidValue;
+    const dim3 grid((a.B * a.Tin + 127) / 128, a.M / 64, nphase);
+    hipLaunchKernelGGL(conv_gemm_tiled_kernel, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.M % 32 || a.Cin % 32 || Ktot % (64 * a.wk)) return hipErrorInvalidValue;
   const int bn = 16 * a.nsub;
   const dim3 grid((a.Tin + bn - 1) / bn, a.M / 32, nphase * a.B);
 #define MX_CG(WK_, NS_)                                                                   \

@@ -8,19 +8,24 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="1x1,4x1,7x1,7x4,7x16,7x32", help="frames x batch list")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
     import torch
     from project_morpheus_amd.engine import SnacDecoder
     from project_morpheus_amd.weights import synthetic_snac_weights
     dec = SnacDecoder(synthetic_snac_weights(), device=0, max_frames=7, max_batch=32)
     st = torch.cuda.Stream()
     out = {}
-    for n, B in ((1, 1), (4, 1), (7, 1), (7, 4), (7, 16), (7, 32)):
+    for n, B in (tuple(int(v) for v in c.split("x")) for c in args.cases.split(",")):
         codes = torch.randint(0, 4096, (B, 7 * n), dtype=torch.int32, device="cuda")
         for _ in range(3):
             dec.decode(codes, seed=1, stream=st)
         st.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 20
+        reps = args.reps
         e0.record(st)
         for i in range(reps):
             dec.decode(codes, seed=i, stream=st)

@@ -78,3 +78,29 @@ def test_device_noise_differs_per_seed(snac_pair):
     _, a2 = dec.decode(codes, want_audio=True, seed=2)
     _, a3 = dec.decode(codes, want_audio=True, seed=1)
     assert not torch.equal(a1, a2) and torch.equal(a1, a3)
+
+
+def test_snac_batched_32_windows_matches_oracle(snac_pair):
+    """The serving shape (B = 32 windows of 7 frames, the block-tiled conv-GEMM path)."""
+    from project_morpheus_amd.engine import SnacDecoder
+    w, _ = snac_pair
+    dec = SnacDecoder(w, device=0, max_frames=7, max_batch=32)
+    n, B = 7, 32
+    rng = np.random.default_rng(4242)
+    codes = rng.integers(0, 4096, size=(B, 7 * n)).astype(np.int32)
+    noise = _noise(B, n, 99)
+    pcm, audio = dec.decode(torch.from_numpy(codes).cuda(), noise=noise.cuda(), want_audio=True)
+    torch.cuda.synchronize()
+    audio = audio.cpu().numpy()
+    pcm = pcm.cpu().numpy()
+    for b in range(0, B, 5):  # every 5th window against the oracle (CPU time)
+        c = codes[b].tolist()
+        c0 = [c[7 * f] for f in range(n)]
+        c1 = [c[7 * f + j] for f in range(n) for j in (1, 4)]
+        c2 = [c[7 * f + j] for f in range(n) for j in (2, 3, 5, 6)]
+        want = snac_ref.decode(w, c0, c1, c2, _split_noise(noise[b], n)).reshape(-1).numpy()
+        rms = float(np.sqrt(np.mean((audio[b] - want) ** 2)))
+        assert rms < 1e-4, (b, rms)
+        assert np.abs(audio[b] - want).max() < 1e-3
+        ref_pcm = (want[2048:4096] * np.float32(32767)).astype(np.int16)
+        assert np.abs(pcm[b].astype(np.int32) - ref_pcm).max() <= 1
