@@ -123,7 +123,7 @@ struct mx_llm {
   int att_nw_b1 = 4, att_nw_batch = 8;
   int o_merge = 1;  // option: one-row o-proj merges the attention splits (0 = ticket merge)  // options: attention waves per block (4 or 8; measured)
   int gemv_wpb = 4;
-  int rows_dbg = 0, rows_npart = 0;  // options: multi-row GEMM experiments / activation parts
+  int rows_lds_pad = 0;              // option: extra LDS KB per multi-row block (occupancy probe)
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
@@ -528,12 +528,11 @@ struct RowSet {
 };
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
-  g.rows_dbg = x->rows_dbg;
+  g.rows_lds_pad = x->rows_lds_pad;
   g.rows_pw = x->rows_pw;
   g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
-  g.rows_npart = x->rows_npart;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
   g.tickets = x->rows_tickets;
@@ -943,12 +942,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
-  } else if (k == "rows_dbg") {
-    if (value < 0 || value > 7) MX_FAIL(x, MX_ERR_ARG, "rows_dbg is a 3-bit experiment mask");
-    x->rows_dbg = value;
-  } else if (k == "rows_npart") {
-    if (value != 0 && value != 2 && value != 3) MX_FAIL(x, MX_ERR_ARG, "rows_npart must be 2 or 3");
-    x->rows_npart = value;
+  } else if (k == "rows_lds_pad") {
+    if (value < 0 || value > 128) MX_FAIL(x, MX_ERR_ARG, "rows_lds_pad must be 0..128 (KB)");
+    x->rows_lds_pad = value;
   } else if (k == "gemv_wpb") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "gemv_wpb must be 4 or 8");
     x->gemv_wpb = value;

@@ -33,8 +33,7 @@ struct GemvArgs {
   size_t ws_floats;
   int* tickets;            // R >= 2 kernel: per-tile arrival counters (zero between launches)
   size_t tickets_n;
-  int rows_dbg;             // R >= 2 kernel timing experiments (0 = product; results invalid otherwise)
-  int rows_npart;          // R >= 2 kernel: activation bf16 parts (2 or 3; 0 = 3)
+  int rows_lds_pad;        // R >= 2 kernel: extra dynamic LDS KB per block (occupancy probe; 0 = none)
   int rows_pw;             // generation 4: weight prefetch distance in sub-chunks (1, 2; 0 = 1)
   int rows_pw_f8;          // the same for e4m3 weights
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
