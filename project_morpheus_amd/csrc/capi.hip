@@ -69,6 +69,8 @@ struct LayerW {
   void* wgu = nullptr;   // [2F][H], rows (gate_i, up_i) interleaved
   void* wd = nullptr;    // [H][F]
   float *sqkv = nullptr, *so = nullptr, *sgu = nullptr, *sd = nullptr;  // fp8 row scales
+  // fragment-major copies for the multi-row GEMM (built at finalize)
+  void *wqkv_f = nullptr, *wo_f = nullptr, *wgu_f = nullptr, *wd_f = nullptr;
   unsigned loaded = 0, scaled = 0;
 };
 
@@ -81,6 +83,8 @@ struct mx_llm {
   void* lm = nullptr;          // lm_head: the embedding (tied bf16) or its own matrix
   float* slm = nullptr;        // fp8 lm_head row scales
   bool lm_loaded = false, lm_scaled = false;
+  void* lm_f = nullptr;        // fragment-major lm_head for the multi-row GEMM
+  int rows_frag = 1;           // option: multi-row GEMMs read the fragment-major copies
   int esz = 2;                 // bytes per matrix element (2 bf16, 1 fp8)
   float* norm = nullptr;
   std::vector<LayerW> L;
@@ -467,6 +471,29 @@ extern "C" int mx_llm_finalize(mx_llm* x) {
   if ((!x->c.tied || f8) && !x->lm_loaded) MX_FAIL(x, MX_ERR_STATE, "lm_head not loaded");
   if (f8 && !x->lm_scaled) MX_FAIL(x, MX_ERR_STATE, "lm_head fp8 scales not loaded");
   if (!x->rope_cos) MX_FAIL(x, MX_ERR_STATE, "rope table not set");
+  // fragment-major copies of every matrix the multi-row GEMM streams (2x the weight bytes
+  // in HBM, 13.2 GB for Orpheus-3B bf16; the one-row GEMVs keep reading the row-major ones)
+  if (!x->lm_f) {
+    MX_TRY(x, hipSetDevice(x->device));
+    const auto& c = x->c;
+    const int H = c.hidden, QD = c.heads * 128, qkv_rows = QD + 2 * c.kv_heads * 128;
+    auto make = [&](const void* src, int N, int K, void** dst) -> hipError_t {
+      void* p = nullptr;
+      hipError_t e = hipMalloc(&p, frag_major_bytes(N, K, x->esz) + 256);
+      if (e != hipSuccess) return e;
+      x->allocs.push_back(p);
+      *dst = p;
+      return launch_frag_major(src, p, N, K, x->esz, nullptr);
+    };
+    for (auto& l : x->L) {
+      MX_TRY(x, make(l.wqkv, qkv_rows, H, &l.wqkv_f));
+      MX_TRY(x, make(l.wo, H, QD, &l.wo_f));
+      MX_TRY(x, make(l.wgu, 2 * c.ffn, H, &l.wgu_f));
+      MX_TRY(x, make(l.wd, H, c.ffn, &l.wd_f));
+    }
+    MX_TRY(x, make(x->lm, c.vocab, H, &x->lm_f));
+    MX_TRY(x, hipDeviceSynchronize());
+  }
   x->final = true;
   return MX_OK;
 }
@@ -570,6 +597,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     g.eps = c.eps;
     // QKV + RoPE + KV append
     g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
+    if (x->rows_frag) g.Wf = l.wqkv_f;
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
     g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
@@ -597,6 +625,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     attach_ws(x, o);
     o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
+    if (x->rows_frag) o.Wf = l.wo_f;
     if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
       if (o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step faster
                                   // than 1 row per wave (fewer partial re-reads)
@@ -613,6 +642,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     attach_ws(x, gu);
     gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.wscale = l.sgu; gu.wdtype = c.wdtype; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
     gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act; gu.force_legacy = x->legacy_gemv; gu.wpb = x->gemv_wpb; gu.rpw = x->rpw_gu;
+    if (x->rows_frag) gu.Wf = l.wgu_f;
     PROF_BEGIN(PK_GU);
     e = launch_gemv(gu, EPI_SILU, true, st);
     PROF_END();
@@ -622,6 +652,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     attach_ws(x, d);
     d.R = rs.R; d.W = l.wd; d.wscale = l.sd; d.wdtype = c.wdtype; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
     d.ystride = H; d.force_legacy = x->legacy_gemv; d.wpb = x->gemv_wpb; d.rpw = x->rpw_down;
+    if (x->rows_frag) d.Wf = l.wd_f;
     PROF_BEGIN(PK_DOWN);
     e = launch_gemv(d, EPI_RESID, false, st);
     PROF_END();
@@ -639,7 +670,7 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot,
   float* lg = x->logits + (size_t)(best - x->best) * c.vocab;
   GemvArgs g{};
   attach_ws(x, g);
-  g.R = R; g.eps = c.eps; g.W = x->lm; g.wscale = x->slm; g.wdtype = c.wdtype; g.N = c.vocab; g.K = c.hidden; g.X = h;
+  g.R = R; g.eps = c.eps; g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype; g.N = c.vocab; g.K = c.hidden; g.X = h;
   g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
   g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = best;
   g.logits = lg; g.logits_all = x->logits_all;
@@ -942,6 +973,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
+  } else if (k == "rows_frag") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
+    x->rows_frag = value;
   } else if (k == "rows_lds_pad") {
     if (value < 0 || value > 128) MX_FAIL(x, MX_ERR_ARG, "rows_lds_pad must be 0..128 (KB)");
     x->rows_lds_pad = value;

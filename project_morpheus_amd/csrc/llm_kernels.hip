@@ -1053,6 +1053,34 @@ hipError_t launch_scatter_rows(void* dst, const void* src, const int32_t* dmap, 
   return hipGetLastError();
 }
 
+// Fragment-major copy of an [N][K] weight matrix for the multi-row GEMM: 16-row tiles, then
+// 128-k sub-chunks, then the WL = 2 esz load instructions of a sub-chunk, then the 64 lanes;
+// lane (c, g) of instruction l holds row 16 t + c, bytes 16 (4 l + g) of the sub-chunk (the
+// same values the row-major addressing gives that lane).  Rows past N repeat row N - 1.
+__global__ void frag_major_kernel(const uint4* src, uint4* dst, int N, int K, int esz) {
+  const int WL = 2 * esz, S = K / 128;
+  const int64_t total = (int64_t)((N + 15) / 16) * S * WL * 64;
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= total) return;
+  const int lane = (int)(u & 63);
+  const int64_t q = u >> 6;  // instruction index
+  const int l = (int)(q % WL);
+  const int64_t ts = q / WL;
+  const int s = (int)(ts % S);
+  const int64_t t = ts / S;
+  const int row = (int)min<int64_t>(16 * t + (lane & 15), N - 1);
+  const int64_t row_units = (int64_t)K * esz / 16;
+  dst[u] = src[(int64_t)row * row_units + (int64_t)s * (8 * esz) + 4 * l + (lane >> 4)];
+}
+
+hipError_t launch_frag_major(const void* src, void* dst, int N, int K, int esz, hipStream_t st) {
+  if (K % 128 || (esz != 1 && esz != 2)) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)((N + 15) / 16) * (K / 128) * 2 * esz * 64;
+  hipLaunchKernelGGL(frag_major_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const uint4*>(src), static_cast<uint4*>(dst), N, K, esz);
+  return hipGetLastError();
+}
+
 hipError_t launch_to_f32(float* dst, const void* src, int64_t n, int src_bf16, hipStream_t st) {
   const int64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(to_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n, src_bf16);

@@ -15,6 +15,7 @@ constexpr int ATT_MERGE_CHUNK = 16; // splits whose partials the merging block p
 
 struct GemvArgs {
   const void* W;           // [N][K] bf16 (WT_BF16) or e4m3 bytes (WT_FP8), packed row order
+  const void* Wf;          // null, or the same matrix fragment-major (launch_frag_major) for R >= 2
   const float* wscale;     // WT_FP8: dequant scale per row [N]
   int wdtype;
   int N, K;
@@ -125,5 +126,8 @@ hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t
 hipError_t launch_scatter_rows(void* dst, const void* src, const int32_t* dmap, int rows,
                                int cols, int mode, hipStream_t st);
 hipError_t launch_to_f32(float* dst, const void* src, int64_t n, int src_bf16, hipStream_t st);
+// [N][K] (esz bytes per element) -> fragment-major copy for the multi-row GEMM (mx_rows_v4.inc)
+hipError_t launch_frag_major(const void* src, void* dst, int N, int K, int esz, hipStream_t st);
+inline size_t frag_major_bytes(int N, int K, int esz) { return (size_t)((N + 15) / 16) * 16 * K * esz; }
 
 }  // namespace mx
