@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
-            "o_merge": 1}
+            "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -27,6 +27,12 @@ VARIANTS = {
     "rpw_down2": {"rpw_down": 2},
     "wpb8": {"gemv_wpb": 8},
     "gu4_down2": {"rpw_gu": 4, "rpw_down": 2},
+    "rowmajor": {"rows_frag": 0},
+    "t128": {"rows_target": 128},
+    "t256": {"rows_target": 256},
+    "t384": {"rows_target": 384},
+    "t512": {"rows_target": 512},
+    "pw1": {"rows_pw": 1},
 }
 
 
