@@ -51,9 +51,9 @@ def parse():
 
 def pmc_traffic(kind):
     """HBM bytes per launch of the one-row GEMV ``kind`` measured by PMC counters in a
-    separate rocprofv3 pass (scripts/pmc_gemv.py, summarised in profiles/r01_pmc_gemv.json);
+    separate rocprofv3 pass (scripts/pmc_gemv.py, summarised in profiles/r02_pmc_gemv.json);
     None when that record is absent."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_gemv.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_gemv.json")
     try:
         with open(path) as fh:
             return json.load(fh)["kernels"][kind]["traffic_bytes"]
@@ -489,7 +489,7 @@ def main():
                          "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
                          "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
                          "traffic": pmc_traffic("gate_up"),
-                         "traffic_source": "profiles/r01_pmc_gemv.json (rocprofv3 --pmc "
+                         "traffic_source": "profiles/r02_pmc_gemv.json (rocprofv3 --pmc "
                                            "FETCH_SIZE / WRITE_SIZE, separate passes)"},
             "eager_step_us_by_kernel": per_step_us,
             "gemv_graph_us": {k: {"us": round(v[0], 2), "GB/s": round(v[1] / v[0] / 1e3, 1)}
