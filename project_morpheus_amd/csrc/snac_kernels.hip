@@ -92,14 +92,21 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, c
   __shared__ float tile[TT + 54][64];
   const float* xb = x + (size_t)bt * T * C + c;
   const float a_in = ain ? ain[c] : 0.f;
-  for (int i = tr; i < TT + 2 * halo; i += 4) {
-    const int t = t0 - halo + i;
-    float v = 0.f;
-    if (t >= 0 && t < T) {
-      v = xb[(size_t)t * C];
-      if (ain) v = snake(v, a_in);
-    }
-    tile[i][cl] = v;
+  // every global load of the haloed tile is issued before any is consumed (a runtime-count
+  // loop of load -> Snake -> LDS store paid one memory latency per row: ~11-15 us per launch
+  // for a single window regardless of its size)
+  constexpr int NI = (TT + 54 + 3) / 4;
+  const int rows = TT + 2 * halo;
+  float v[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tr + 4 * j, t = t0 - halo + i;
+    v[j] = (i < rows && t >= 0 && t < T) ? xb[(size_t)t * C] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tr + 4 * j;
+    if (i < rows) tile[i][cl] = ain ? snake(v[j], a_in) : v[j];
   }
   __syncthreads();
   float wk[7];
