@@ -312,16 +312,20 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
 // fragment order, so every operand byte fetched from L2 feeds 4-8x more MFMAs than the
 // one-wave kernels above (whose A / X re-fetches made them vector-memory bound: 50-70 TF/s).
 // The next step's global loads are in flight (registers) while this step's MFMAs run.
-// Grid (ceil(B*Tin / 128), M / 64, nphase).
+// Grid (M / 64 * nphase, ceil(B*Tin / 128)).
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int wm = w & 1, wn = w >> 1;  // wave position in the 2 x 2 block
-  const int ph = blockIdx.z;
-  const int m0 = blockIdx.y * 64;
+  // blockIdx.x enumerates (M tile, phase) fastest, so the blocks that read one X column tile
+  // are dispatched together and share it through L2 (an X tile is read by M/64 x nphase
+  // blocks: 64 for the first ConvTranspose)
+  const int mtiles = a.M / 64;
+  const int ph = blockIdx.x / mtiles;
+  const int m0 = (blockIdx.x - ph * mtiles) * 64;
   const int ncol = a.B * a.Tin;
-  const int col0 = blockIdx.x * 128;
+  const int col0 = blockIdx.y * 128;
   const uint16_t* A = a.Abf[ph];
   const int Ktot = a.nseg * a.Cin;
   const size_t plane = (size_t)a.M * Ktot;
@@ -537,7 +541,9 @@ hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
   const int Ktot = a.nseg * a.Cin;
   if (a.tiled) {
     if (a.M % 64 || a.Cin % 32) return hipErrorInvalidValue;
-    const dim3 grid((a.B * a.Tin + 127) / 128, a.M / 64, nphase);
+    const int ctiles = (a.B * a.Tin + 127) / 128;
+    if (ctiles > 65535) return hipErrorInvalidValue;
+    const dim3 grid(a.M / 64 * nphase, ctiles);
     hipLaunchKernelGGL(conv_gemm_tiled_kernel, grid, dim3(256), 0, st, a);
     return hipGetLastError();
   }
