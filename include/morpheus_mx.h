@@ -83,6 +83,9 @@ int mx_llm_set_weight(mx_llm* ctx, const char* name, const void* dev_data, int64
                       int dtype);
 /* RoPE tables [n_pos][head_dim/2] fp32 (host memory), llama3-scaled frequencies. */
 int mx_llm_set_rope(mx_llm* ctx, const float* cos_host, const float* sin_host, int n_pos);
+/* Checks every weight is present and builds the fragment-major copies the multi-row GEMM
+ * streams (2x the matrix bytes in HBM).  Weights are frozen afterwards: mx_llm_set_weight
+ * then returns MX_ERR_STATE. */
 int mx_llm_finalize(mx_llm* ctx);
 /* Prefill prompt ids (host) into `slot`, bind the slot to decode row `row`, set the slot's
  * generation parameters, pick the first token.  Enqueued on `stream`. */

@@ -376,6 +376,8 @@ extern "C" int mx_llm_set_weight(mx_llm* x, const char* name, const void* data, 
   if (!x || !name || !data) return MX_ERR_ARG;
   if (dtype != MX_DTYPE_F32 && dtype != MX_DTYPE_BF16 && dtype != MX_DTYPE_FP8)
     MX_FAIL(x, MX_ERR_ARG, "bad dtype");
+  // finalize derived the fragment-major copies and captured graphs from these weights
+  if (x->final) MX_FAIL(x, MX_ERR_STATE, "weights are frozen after mx_llm_finalize");
   MX_TRY(x, hipSetDevice(x->device));
   const auto& c = x->c;
   const int H = c.hidden;

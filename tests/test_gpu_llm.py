@@ -131,6 +131,11 @@ def test_bad_args_fail_loudly():
     bad.pop("l1.wd")
     with pytest.raises(_lib.MxError):
         LlmEngine(cfg, bad, max_slots=1, max_pos=128)   # incomplete weights
+    # weights are frozen once finalize built the fragment-major copies
+    import ctypes
+    t = w["norm"].float().cuda().contiguous()
+    rc = eng.lib.mx_llm_set_weight(eng.h, b"norm", ctypes.c_void_p(t.data_ptr()), t.numel(), 0)
+    assert rc == -3, rc  # MX_ERR_STATE
 
 
 def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=None,
