@@ -40,7 +40,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import STOP_IDS
+from .config import SNAC_MAX_HOLD, SNAC_MIN_BATCH, STOP_IDS
 from .engine import SAMPLES_PER_FRAME, SLICE_HI, SLICE_LO, LlmEngine, SnacDecoder
 from .schedule import WindowScheduler, code_of_id
 
@@ -172,10 +172,17 @@ class TokenHandle(StreamHandle):
 
 
 class BatchSynthesizer:
-    def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: int = 2, seed: int = 0):
+    def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: int = 2, seed: int = 0,
+                 snac_min_batch: Optional[int] = None, snac_max_hold: Optional[int] = None):
         if llm.max_slots < llm.max_batch:
             raise ValueError("BatchSynthesizer needs one KV slot per decode row")
         self.llm, self.snac, self.depth, self.seed = llm, snac, depth, seed
+        # SNAC window coalescing: due windows are held until `snac_min_batch` of them are
+        # ready or the oldest has waited `snac_max_hold` decode steps (a stream's first window
+        # and closing streams' windows go at once).  Staggered streams make ~streams / 7
+        # windows due per step; a bigger SNAC batch costs less per window.
+        self.snac_min_batch = max(1, SNAC_MIN_BATCH if snac_min_batch is None else snac_min_batch)
+        self.snac_max_hold = max(0, SNAC_MAX_HOLD if snac_max_hold is None else snac_max_hold)
         self.stream = torch.cuda.Stream(llm.device)
         self.snac_stream = torch.cuda.Stream(llm.device)
         self.ring = _BatchRing(16, snac.max_batch, snac.max_frames)
@@ -290,6 +297,8 @@ class BatchSynthesizer:
         inflight: Deque = deque()   # (event, [(row, req, k)])
         pending: Deque = deque()    # (event, ring index, [(req, nbytes)])
         closing: Deque = deque()    # streams whose end waits for their last SNAC call
+        held: List = []             # due SNAC windows not launched yet (coalescing)
+        held_age = [0]              # decode steps the oldest held window has waited
         live = self._live
 
         def now():
@@ -456,8 +465,14 @@ class BatchSynthesizer:
             for r in rows:
                 if r.req is not None and r.stopped:
                     finish(r, due)
-            if due:
-                launch_windows(due)
+            if held:
+                held_age[0] += 1
+            held.extend(due)
+            if held and (len(held) >= self.snac_min_batch or held_age[0] >= self.snac_max_hold or
+                         closing or any(w == 0 for _, w, _ in held) or not inflight):
+                launch_windows(held)
+                held.clear()
+                held_age[0] = 0
             drain(block=False)
             announce()
         for e, _ in inflight:

@@ -114,6 +114,11 @@ MX_DEVICE = env_int("MORPHEUS_MX_DEVICE", 0)
 MX_MAX_POS = env_int("MORPHEUS_MX_MAX_POS", env_int("LLAMA_N_CTX", 8192))
 MX_MAX_SLOTS = env_int("MORPHEUS_MX_MAX_SLOTS", 8)
 MX_GPUS = env_int("MORPHEUS_MX_GPUS", 1)                # worker processes (one per GPU)
+# batched SNAC window coalescing (batching.BatchSynthesizer): launch when this many windows
+# are due, or when the oldest has waited SNAC_MAX_HOLD decode steps (12 / 2 measured: configs[2]
+# 96.8 -> 99.2x, p50 first audio +1.4 ms; profiles/r02_bench_snac_coalescing.log)
+SNAC_MIN_BATCH = env_int("MORPHEUS_MX_SNAC_MIN_BATCH", 12)
+SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
 
 
 def synthetic_audio_ids(n: int, seed: int):
