@@ -128,7 +128,7 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
 
     from project_morpheus_amd import inference as I
     from project_morpheus_amd.batching import BatchSynthesizer, StreamRequest
-    syn = BatchSynthesizer(llm, snac, depth=2, seed=rank)
+    syn = BatchSynthesizer(llm, snac, seed=rank)
     rng = np.random.default_rng(4 + 1000 * rank)
 
     def requests():
@@ -258,7 +258,7 @@ def run_long_read(args, llm, snac, rank, world, dist):
     from project_morpheus_amd.tokenizer import Tokenizer
     docs = S.long_read_documents(args.long_read_docs, 3000, seed=5)
     jobs = S.plan_jobs(docs, Tokenizer(None).encode, "tara", args.max_tokens)
-    syn = BatchSynthesizer(llm, snac, depth=2, seed=rank)
+    syn = BatchSynthesizer(llm, snac, seed=rank)
     job_index = {id(j): i for i, j in enumerate(jobs)}
 
     def synthesize(mine):

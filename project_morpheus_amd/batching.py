@@ -40,7 +40,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import SNAC_MAX_HOLD, SNAC_MIN_BATCH, STOP_IDS
+from .config import BATCH_DEPTH, SNAC_MAX_HOLD, SNAC_MIN_BATCH, STOP_IDS
 from .engine import SAMPLES_PER_FRAME, SLICE_HI, SLICE_LO, LlmEngine, SnacDecoder
 from .schedule import WindowScheduler, code_of_id
 
@@ -172,11 +172,12 @@ class TokenHandle(StreamHandle):
 
 
 class BatchSynthesizer:
-    def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: int = 2, seed: int = 0,
+    def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: Optional[int] = None, seed: int = 0,
                  snac_min_batch: Optional[int] = None, snac_max_hold: Optional[int] = None):
         if llm.max_slots < llm.max_batch:
             raise ValueError("BatchSynthesizer needs one KV slot per decode row")
-        self.llm, self.snac, self.depth, self.seed = llm, snac, depth, seed
+        self.llm, self.snac, self.seed = llm, snac, seed
+        self.depth = max(1, BATCH_DEPTH if depth is None else depth)
         # SNAC window coalescing: due windows are held until `snac_min_batch` of them are
         # ready or the oldest has waited `snac_max_hold` decode steps (a stream's first window
         # and closing streams' windows go at once).  Staggered streams make ~streams / 7

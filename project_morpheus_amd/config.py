@@ -117,6 +117,8 @@ MX_GPUS = env_int("MORPHEUS_MX_GPUS", 1)                # worker processes (one 
 # batched SNAC window coalescing (batching.BatchSynthesizer): launch when this many windows
 # are due, or when the oldest has waited SNAC_MAX_HOLD decode steps (12 / 2 measured: configs[2]
 # 96.8 -> 99.2x, p50 first audio +1.4 ms; profiles/r02_bench_snac_coalescing.log)
+# decode steps the batcher keeps queued ahead of the host (batching.BatchSynthesizer)
+BATCH_DEPTH = env_int("MORPHEUS_MX_BATCH_DEPTH", 2)
 SNAC_MIN_BATCH = env_int("MORPHEUS_MX_SNAC_MIN_BATCH", 12)
 SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
 
