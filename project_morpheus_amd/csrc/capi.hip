@@ -1265,7 +1265,7 @@ static int snac_tiled_min_batch() {
 }
 
 static void pick_tiles(ConvGemmArgs& g, int nphase) {
-  g.tiled = g.M % 64 == 0 && g.B >= snac_tiled_min_batch();
+  g.tiled = g.M % 64 == 0 && g.B >= snac_tiled_min_batch() ? 1 : 0;
   g.nsub = g.Tin >= 2048 ? 4 : 2;
   const int tiles = (g.M / 32) * ((g.Tin + 16 * g.nsub - 1) / (16 * g.nsub)) * nphase * g.B;
   const int Ktot = g.nseg * g.Cin;

@@ -306,34 +306,35 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
 
 // ---------------------------------------------------------------------------------
 // Block-tiled conv-GEMM for batched windows (the serving shapes): the B windows' columns are
-// concatenated (column = window * Tin + t), and a 256-thread block computes a 64 x 128 tile
-// over 2 x 2 waves (32 x 64 each).  Per 32-deep k step the block stages A (64 rows x 3 bf16
-// planes) and X (128 columns x 32 channels, split into 3 bf16 parts) ONCE in LDS in MFMA
-// fragment order, so every operand byte fetched from L2 feeds 4-8x more MFMAs than the
-// one-wave kernels above (whose A / X re-fetches made them vector-memory bound: 50-70 TF/s).
-// The next step's global loads are in flight (registers) while this step's MFMAs run.
-// Grid (M / 64 * nphase, ceil(B*Tin / 128)).
+// concatenated (column = window * Tin + t), and a 256-thread block computes a (64 BMT) x 128
+// tile: BMT = 1 over 2 x 2 waves (32 x 64 each), BMT = 2 over 4 x 1 waves (32 x 128 each:
+// the staged X tile feeds twice the MFMAs).  Per 32-deep k step the block stages A (64 BMT
+// rows x 3 bf16 planes) and X (128 columns x 32 channels, split into 3 bf16 parts) ONCE in
+// LDS in MFMA fragment order, so every operand byte fetched from L2 feeds 4-16x more MFMAs
+// than the one-wave kernels above (whose A / X re-fetches made them vector-memory bound:
+// 50-70 TF/s).  The next step's global loads are in flight (registers) while this step's
+// MFMAs run.  Grid (M / (64 BMT) * nphase, ceil(B*Tin / 128)): (M tile, phase) fastest, so
+// the blocks reading one X column tile are dispatched together and share it through L2.
 // ---------------------------------------------------------------------------------
+template <int BMT>
 __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
+  constexpr int WMN = 2 * BMT, NJ = 2 * WMN;  // waves along M (of 4); n-tiles per wave (of 8)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
-  const int wm = w & 1, wn = w >> 1;  // wave position in the 2 x 2 block
-  // blockIdx.x enumerates (M tile, phase) fastest, so the blocks that read one X column tile
-  // are dispatched together and share it through L2 (an X tile is read by M/64 x nphase
-  // blocks: 64 for the first ConvTranspose)
-  const int mtiles = a.M / 64;
+  const int wm = w % WMN, wn = w / WMN;
+  const int mtiles = a.M / (64 * BMT);
   const int ph = blockIdx.x / mtiles;
-  const int m0 = (blockIdx.x - ph * mtiles) * 64;
+  const int m0 = (blockIdx.x - ph * mtiles) * 64 * BMT;
   const int ncol = a.B * a.Tin;
   const int col0 = blockIdx.y * 128;
   const uint16_t* A = a.Abf[ph];
   const int Ktot = a.nseg * a.Cin;
   const size_t plane = (size_t)a.M * Ktot;
   const int d0 = a.dph[ph][0], d1 = a.dph[ph][1];
-  __shared__ uint4 As[3][4][64];    // [plane][m-tile][lane]: A fragments
-  __shared__ uint4 Bs[3][8][64];    // [part][n-tile][lane]: B fragments
+  __shared__ uint4 As[3][4 * BMT][64];  // [plane][m-tile][lane]: A fragments
+  __shared__ uint4 Bs[3][8][64];        // [part][n-tile][lane]: B fragments
 
-  // staging roles: A — row ar = tid / 4, k quarter aq = tid % 4 (8 k, 16 B per plane);
+  // staging roles: A — rows ar + 64 r, k quarter aq (8 k, 16 B per plane);
   // X — column xn = tid / 2, channel half xh = tid % 2 (16 channels, 4 x float4)
   const int ar = tid >> 2, aq = tid & 3;
   const uint16_t* Arow = A + (size_t)(m0 + ar) * Ktot + 8 * aq;
@@ -342,11 +343,14 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
   const bool xin = xcol < ncol;
   const int xbt = xin ? xcol / a.Tin : 0, xt = xin ? xcol - xbt * a.Tin : 0;
   const float* Xw = a.X + (size_t)xbt * a.Tin * a.Cin;
-  uint4 ra[3];
+  uint4 ra[BMT][3];
   float4 rx[4];
   auto gload = [&](int kc) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) ra[p] = *reinterpret_cast<const uint4*>(Arow + p * plane + kc);
+    for (int r = 0; r < BMT; ++r)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        ra[r][p] = *reinterpret_cast<const uint4*>(Arow + (size_t)64 * r * Ktot + p * plane + kc);
     const int seg = kc >= a.Cin ? 1 : 0;
     const int t = xt + (seg ? d1 : d0);
     const bool ok = xin && t >= 0 && t < a.Tin;
@@ -357,7 +361,9 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
   };
   auto lstore = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) As[p][ar >> 4][aq * 16 + (ar & 15)] = ra[p];
+    for (int r = 0; r < BMT; ++r)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) As[p][4 * r + (ar >> 4)][aq * 16 + (ar & 15)] = ra[r][p];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // 8 channels = k group g' = 2 xh + h of column xn
       float x[8] = {rx[2 * h].x, rx[2 * h].y, rx[2 * h].z, rx[2 * h].w,
@@ -370,38 +376,38 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
     }
   };
 
-  f32x4 acc[2][4];
+  f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   gload(0);
   for (int kc = 0; kc < Ktot; kc += 32) {
     __syncthreads();  // the previous step's fragments are consumed
     lstore();
     __syncthreads();
     if (kc + 32 < Ktot) gload(kc + 32);
-    bf16x8 af[2][3], bfr[4][3];
+    bf16x8 af[2][3];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int p = 0; p < 3; ++p) af[i][p] = __builtin_bit_cast(bf16x8, As[p][2 * wm + i][lane]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) bfr[j][p] = __builtin_bit_cast(bf16x8, Bs[p][4 * wn + j][lane]);
     constexpr int PA[6] = {1, 0, 2, 0, 1, 0}, PB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
+    for (int j = 0; j < NJ; ++j) {
+      bf16x8 bfr[3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int p = 0; p < 3; ++p) bfr[p] = __builtin_bit_cast(bf16x8, Bs[p][NJ * wn + j][lane]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][PA[q]], bfr[j][PB[q]], acc[i][j], 0, 0, 0);
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][PA[q]], bfr[PB[q]], acc[i][j], 0, 0, 0);
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = col0 + 64 * wn + 16 * j + c;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = col0 + 16 * (NJ * wn + j) + c;
     if (col >= ncol) continue;
     const int bt = col / a.Tin, t = col - bt * a.Tin;
 #pragma unroll
@@ -543,8 +549,9 @@ hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
     if (a.M % 64 || a.Cin % 32) return hipErrorInvalidValue;
     const int ctiles = (a.B * a.Tin + 127) / 128;
     if (ctiles > 65535) return hipErrorInvalidValue;
-    const dim3 grid(a.M / 64 * nphase, ctiles);
-    hipLaunchKernelGGL(conv_gemm_tiled_kernel, grid, dim3(256), 0, st, a);
+    // BMT = 2 (128 x 128 blocks) is parity-green but slower: 0.101 vs 0.098 ms per window at
+    // x32, 0.164 vs 0.138 at x8 (occupancy 2 vs 4; profiles/r02_snac_tile_bm.log)
+    hipLaunchKernelGGL(conv_gemm_tiled_kernel<1>, dim3(a.M / 64 * nphase, ctiles), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (a.M % 32 || a.Cin % 32 || Ktot % (64 * a.wk)) return hipErrorInvalidValue;
