@@ -322,11 +322,21 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int wm = w % WMN, wn = w / WMN;
+  // XCD-aware tile order: the dispatcher deals consecutive block ids round-robin over the 8
+  // XCDs, each with its own L2, so the gridDim.x blocks of one X column tile would land on
+  // different XCDs and each fetch the tile from HBM.  Logical id = XCD-major over the first
+  // 8 * (nb / 8) ids (a bijection; the tail keeps its id): one XCD runs consecutive logical
+  // ids, i.e. all (M tile, phase) blocks of a column tile, and the tile is read once.
+  const int nb = gridDim.x * gridDim.y;
+  int bid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int per = nb >> 3;
+  if (bid < per * 8) bid = (bid & 7) * per + (bid >> 3);
+  const int bx = bid % gridDim.x, by = bid / gridDim.x;
   const int mtiles = a.M / (64 * BMT);
-  const int ph = blockIdx.x / mtiles;
-  const int m0 = (blockIdx.x - ph * mtiles) * 64 * BMT;
+  const int ph = bx / mtiles;
+  const int m0 = (bx - ph * mtiles) * 64 * BMT;
   const int ncol = a.B * a.Tin;
-  const int col0 = blockIdx.y * 128;
+  const int col0 = by * 128;
   const uint16_t* A = a.Abf[ph];
   const int Ktot = a.nseg * a.Cin;
   const size_t plane = (size_t)a.M * Ktot;
