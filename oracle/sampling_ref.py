@@ -10,7 +10,8 @@ select (csrc/sample_kernels.hip), by sorting:
   e_i = exp((l_i - max l) / T) (float32), f_i = floor(e_i * 2^40) (uint64),
   Z = sum f_i, thr = max(1, floor(float64(Z) * top_p)) (Z when top_p >= 1),
   keep i iff sum_{j: e_j > e_i} f_j < thr,
-  u_i = ((philox4x32_10(key=seed, ctr=(i, pos, 0, 0)).x0 >> 8) + 0.5) * 2^-24,
+  u_i = ((philox4x32_10(key=seed, ctr=(i, pos, 0, 0)).x0 >> 9) + 0.5) * 2^-23  (exact in
+        float32, so 0 < u_i < 1: a 24-bit draw rounded to 1.0 would lose the race),
   token = argmax over kept i of e_i / -log(u_i)   (smallest index on ties).
 
 Greedy (temperature <= 0) is argmax of the penalised logits.  Parity unpinned against vLLM /
@@ -78,7 +79,7 @@ def sample(logits: np.ndarray, temperature: float, top_p: float, seed: int, pos:
     e, kept, _, _ = nucleus(lg, temperature, top_p)
     idx = np.nonzero(kept)[0]
     x = philox_x0(idx, pos, seed)
-    u = ((x >> 8).astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -24)
+    u = ((x >> 9).astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -23)
     s = e[idx] / -np.log(u)
     best = int(np.argmax(s))          # first index among equal maxima = smallest token id
     tok = int(idx[best])

@@ -27,8 +27,15 @@ class MxUnavailable(RuntimeError):
     pass
 
 
+MX_ERR_ARG, MX_ERR_HIP, MX_ERR_STATE, MX_ERR_OOM = -1, -2, -3, -4
+
+
 class MxError(RuntimeError):
-    pass
+    """A non-zero return of the C ABI; ``rc`` is the MX_ERR_* code."""
+
+    def __init__(self, msg: str, rc: int = 0):
+        super().__init__(msg)
+        self.rc = rc
 
 
 class LlmConfig(C.Structure):
@@ -107,7 +114,7 @@ def load(path: str = LIB_PATH):
 def check(rc: int, err_fn, handle) -> None:
     if rc != 0:
         msg = err_fn(handle)
-        raise MxError(f"morpheus_mx error {rc}: {msg.decode() if msg else ''}")
+        raise MxError(f"morpheus_mx error {rc}: {msg.decode() if msg else ''}", rc)
 
 
 def require_gpu() -> None:

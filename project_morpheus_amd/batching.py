@@ -94,6 +94,24 @@ class StreamRequest:
         self.cancelled = True
 
 
+def check_params(penalty: float, temperature: float, top_p: float, max_tokens: int) -> None:
+    """Reject generation parameters the device cannot run (mx_llm_prefill returns MX_ERR_ARG
+    for them): a bad request must fail alone, at submit time, never inside the GPU loop."""
+    import math
+    for name, v in (("repetition_penalty", penalty), ("temperature", temperature),
+                    ("top_p", top_p)):
+        if not isinstance(v, (int, float)) or not math.isfinite(v):
+            raise ValueError(f"{name} must be a finite number, got {v!r}")
+    if penalty <= 0:
+        raise ValueError(f"repetition_penalty must be > 0, got {penalty}")
+    if temperature < 0:
+        raise ValueError(f"temperature must be >= 0, got {temperature}")
+    if not 0 < top_p <= 1:
+        raise ValueError(f"top_p must be in (0, 1], got {top_p}")
+    if not isinstance(max_tokens, int) or max_tokens < 1:
+        raise ValueError(f"max_tokens must be a positive integer, got {max_tokens!r}")
+
+
 class _Row:
     def __init__(self, idx: int):
         self.idx = idx
@@ -238,6 +256,7 @@ class BatchSynthesizer:
         return self
 
     def submit(self, req: StreamRequest) -> StreamHandle:
+        check_params(req.penalty, req.temperature, req.top_p, req.max_tokens)
         if self._thread is None:
             self.start()
         h = StreamHandle(req) if req.audio else TokenHandle(req)
@@ -337,13 +356,21 @@ class BatchSynthesizer:
                 if req.noise_seed is None:
                     req.noise_seed = (self.seed * 1000003 + self._admitted) & _MASK48
                 self._admitted += 1
+                try:  # a request the device rejects fails alone; the loop serves on
+                    check_params(req.penalty, req.temperature, req.top_p, req.max_tokens)
+                    llm.prefill(r.idx, r.idx, req.prompt_ids, req.penalty, self.stream,
+                                temperature=req.temperature, top_p=req.top_p, seed=req.seed)
+                except (ValueError, _lib.MxError) as e:
+                    if isinstance(e, _lib.MxError) and e.rc != _lib.MX_ERR_ARG:
+                        raise  # a device failure is not this request's fault
+                    req.error = e
+                    complete(req)
+                    continue
                 r.req, r.sched, r.n0 = req, WindowScheduler(), n0
                 r.limit = max(1, min(req.max_tokens, llm.max_pos - n0))
                 r.issued, r.stopped, r.parked = 1, False, False
                 req.t_admit = now()
                 live.append(req)
-                llm.prefill(r.idx, r.idx, req.prompt_ids, req.penalty, self.stream,
-                            temperature=req.temperature, top_p=req.top_p, seed=req.seed)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 inflight.append((ev, [(r, req, 0)]))

@@ -48,11 +48,19 @@ def sse_event(cid: str, created: int, model: str, text: str, finish: Optional[st
 
 
 def params_from_payload(p: Dict[str, Any]) -> Dict[str, Any]:
-    return {"max_tokens": int(p.get("max_tokens") or I.MAX_TOKENS),
-            "temperature": float(p.get("temperature", I.TEMPERATURE)),
-            "top_p": float(p.get("top_p", I.TOP_P)),
-            "penalty": float(p.get("repeat_penalty", p.get("repetition_penalty",
-                                                           I.REPETITION_PENALTY)))}
+    """Generation parameters of a request; ValueError (HTTP 400) for values the engine
+    cannot run (non-numbers, temperature < 0, top_p outside (0, 1], penalty <= 0)."""
+    from .batching import check_params
+    try:
+        out = {"max_tokens": int(p.get("max_tokens") or I.MAX_TOKENS),
+               "temperature": float(p.get("temperature", I.TEMPERATURE)),
+               "top_p": float(p.get("top_p", I.TOP_P)),
+               "penalty": float(p.get("repeat_penalty", p.get("repetition_penalty",
+                                                              I.REPETITION_PENALTY)))}
+    except (TypeError, ValueError) as e:
+        raise ValueError(f"bad generation parameter: {e}") from e
+    check_params(out["penalty"], out["temperature"], out["top_p"], out["max_tokens"])
+    return out
 
 
 async def next_token(handle, poll_s: float = 0.002):
@@ -79,10 +87,13 @@ def build_route(token_source: Callable[..., Any], encode: Callable[[str], List[i
         prompt = payload.get("prompt")
         if not isinstance(prompt, str) or not prompt:
             return JSONResponse({"error": "missing prompt"}, status_code=400)
-        params = params_from_payload(payload)
+        try:
+            params = params_from_payload(payload)
+            ids = prompt_ids_from_text(prompt, encode)
+            handle = token_source(ids, **params)
+        except ValueError as e:  # rejected before it reaches the GPU loop
+            return JSONResponse({"error": str(e)}, status_code=400)
         model = str(payload.get("model", "orpheus-mi355x"))
-        ids = prompt_ids_from_text(prompt, encode)
-        handle = token_source(ids, **params)
         cid, created = f"cmpl-{id(handle):x}", int(time.time())
 
         async def events():

@@ -121,6 +121,23 @@ MX_GPUS = env_int("MORPHEUS_MX_GPUS", 1)                # worker processes (one 
 BATCH_DEPTH = env_int("MORPHEUS_MX_BATCH_DEPTH", 2)
 SNAC_MIN_BATCH = env_int("MORPHEUS_MX_SNAC_MIN_BATCH", 12)
 SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
+# Random streams of a request given no seed (sampling + SNAC noise): 0 (default) draws a fresh
+# 64-bit seed per request, as vLLM SamplingParams(seed=None) and llama.cpp's default do, so
+# "regenerate" gives new audio; 1 derives it from the prompt ids (reproducible bench / parity
+# runs: the same text gives the same audio whatever the batch company or arrival order).
+CONTENT_SEED = env_int("MORPHEUS_MX_CONTENT_SEED", 0)
+
+
+def request_seed(prompt_ids, seed=None) -> int:
+    """The seed of one request: ``seed`` if given, else content-derived (CONTENT_SEED=1) or a
+    fresh random 64-bit value."""
+    if seed is not None:
+        return int(seed)
+    if CONTENT_SEED:
+        import zlib
+        return zlib.crc32(np.asarray(prompt_ids, dtype=np.int32).tobytes())
+    import secrets
+    return secrets.randbits(64)
 
 
 def synthetic_audio_ids(n: int, seed: int):

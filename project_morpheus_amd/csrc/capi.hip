@@ -117,6 +117,7 @@ struct mx_llm {
   std::map<int, hipGraphExec_t> graphs;   // key: n_rows * 4096 + attention splits
   std::vector<int> pos_mirror;            // host copy of row_pos (position of next token)
   std::vector<char> row_active;
+  std::vector<char> row_samples;          // row's slot samples (temperature > 0): head runs the sampler
   std::map<int, hipGraph_t> graph_defs;
   bool final = false;
   int max_rows = 0;
@@ -174,6 +175,7 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   x->L.resize(c.layers);
   x->pos_mirror.assign(c.max_batch, 0);
   x->row_active.assign(c.max_batch, 0);
+  x->row_samples.assign(c.max_batch, 0);
   x->max_rows = c.max_batch > c.max_prefill ? c.max_batch : c.max_prefill;
   x->nsplit_max = c.max_pos / ATT_S_MIN;
   const int qkv_rows = c.heads * 128 + 2 * c.kv_heads * 128;
@@ -662,12 +664,12 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
   return e;
 }
 
-// lm_head + penalty + argmax for R rows, then the sampler for the rows whose slot samples
-// (greedy rows return at once).  `best` points into x->best; its offset selects the rows of
-// x->logits used.
+// lm_head + penalty + argmax for R rows, then -- only when one of them samples -- the
+// sampler (greedy rows return at once).  `best` points into x->best; its offset selects the
+// rows of x->logits used.
 static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot,
                                const int32_t* pos, int R, unsigned long long* best,
-                               hipStream_t st) {
+                               bool sample, hipStream_t st) {
   const auto& c = x->c;
   float* lg = x->logits + (size_t)(best - x->best) * c.vocab;
   GemvArgs g{};
@@ -677,7 +679,7 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot,
   g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = best;
   g.logits = lg; g.logits_all = x->logits_all;
   hipError_t e = launch_gemv(g, EPI_ARGMAX, true, st);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !sample) return e;  // all-greedy steps carry no sampler node
   SampleArgs sa{};
   sa.logits = lg; sa.row_slot = slot; sa.row_pos = pos; sa.temp = x->samp_temp;
   sa.top_p = x->samp_top_p; sa.seed = x->samp_seed; sa.best = best; sa.V = c.vocab;
@@ -699,8 +701,14 @@ static int att_nw_of(const mx_llm* x, int R, int max_len) {
   return nw;
 }
 
-static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hipStream_t st,
-                                 Prof* prof) {
+static bool any_samples(const mx_llm* x, int n_rows) {
+  for (int r = 0; r < n_rows; ++r)
+    if (x->row_samples[r]) return true;
+  return false;
+}
+
+static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, bool sample,
+                                 hipStream_t st, Prof* prof) {
   const auto& c = x->c;
   const int nw = att_nw_of(x, n_rows, max_len);
   const int S = 32 * nw * cpw;
@@ -708,7 +716,8 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, hi
             (max_len + S - 1) / S};
   hipError_t e = enqueue_layers(x, rs, st, prof);
   PROF_BEGIN(PK_HEAD);
-  if (e == hipSuccess) e = enqueue_head(x, x->h_dec, x->row_slot, x->row_pos, n_rows, x->best, st);
+  if (e == hipSuccess)
+    e = enqueue_head(x, x->h_dec, x->row_slot, x->row_pos, n_rows, x->best, sample, st);
   PROF_END();
   PROF_BEGIN(PK_COMMIT);
   if (e == hipSuccess) {
@@ -751,7 +760,7 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
   MX_TRY(x, enqueue_head(x, x->h_pre + (size_t)(n - 1) * c.hidden, x->pre_slot + (n - 1),
-                         x->pre_pos + (n - 1), 1, x->best + row, st));
+                         x->pre_pos + (n - 1), 1, x->best + row, sp->temperature > 0.f, st));
   // bind decode row -> slot at position n-1, then commit (advances to n)
   MX_TRY(x, launch_set_rows(x->row_slot + row, x->row_pos + row, 1, slot, n - 1, st));
   CommitArgs cm{};
@@ -762,6 +771,7 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, launch_commit(cm, 1, st));
   x->pos_mirror[row] = n;
   x->row_active[row] = 1;
+  x->row_samples[row] = sp->temperature > 0.f ? 1 : 0;
   return MX_OK;
 }
 
@@ -792,13 +802,15 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   const int nw = att_nw_of(x, n_rows, ml);
   const int S = 32 * cpw * nw;
   const int nsplit = (ml + S - 1) / S;
-  // (chunks and waves are part of the key: one nsplit can come from several shapes)
-  const int key = ((n_rows * 16 + cpw) * 16 + nw) * 4096 + nsplit;
+  // (chunks and waves are part of the key: one nsplit can come from several shapes; so is
+  // whether any row samples: all-greedy graphs have no sampler node)
+  const bool sample = any_samples(x, n_rows);
+  const int key = (((n_rows * 16 + cpw) * 16 + nw) * 4096 + nsplit) * 2 + (sample ? 1 : 0);
   auto it = x->graphs.find(key);
   if (it == x->graphs.end()) {
     MX_TRY(x, hipStreamSynchronize(st));
     MX_TRY(x, hipStreamBeginCapture(x->cap, hipStreamCaptureModeRelaxed));
-    hipError_t e = enqueue_decode(x, n_rows, nsplit * S, cpw, x->cap, nullptr);
+    hipError_t e = enqueue_decode(x, n_rows, nsplit * S, cpw, sample, x->cap, nullptr);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(x->cap, &g);
     MX_TRY(x, e);
@@ -823,7 +835,8 @@ extern "C" int mx_llm_decode_profiled(mx_llm* x, int n_rows, void* stream,
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   Prof prof;
   const int ml = decode_max_len(x, n_rows);
-  hipError_t e = enqueue_decode(x, n_rows, ml, att_cpw_auto(x, n_rows, ml), st, &prof);
+  hipError_t e = enqueue_decode(x, n_rows, ml, att_cpw_auto(x, n_rows, ml), any_samples(x, n_rows),
+                                st, &prof);
   mirror_step(x, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   for (auto& p : prof.ev) {
@@ -1029,6 +1042,7 @@ extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
                             (hipStream_t)stream));
   x->pos_mirror[row] = 0;
   x->row_active[row] = 0;
+  x->row_samples[row] = 0;
   return MX_OK;
 }
 

@@ -13,7 +13,8 @@
 //   f_i   = floor(e_i * 2^40)                             integer mass (uint64, exact sums)
 //   Z     = sum f_i;   thr = max(1, floor(top_p * Z)) in float64 (top_p >= 1: thr = Z)
 //   keep i  iff  sum_{j : e_j > e_i} f_j < thr            (nucleus; ties kept together)
-//   u_i   = ((philox(seed, (i, pos)).x >> 8) + 0.5) * 2^-24,   q_i = -log(u_i)
+//   u_i   = ((philox(seed, (i, pos)).x >> 9) + 0.5) * 2^-23,   q_i = -log(u_i)
+//           (23 bits: u + 0.5 is exact in fp32, so u is strictly inside (0, 1))
 //   token = argmax_{kept i} e_i / q_i  (smallest index on ties)   -- the exponential race,
 //           an exact draw from the renormalised kept distribution.
 // Integer masses make the nucleus cut order-independent (deterministic under atomics); the
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(SMP_T) void sample_kernel(SampleArgs a) {
     const float e = e_of(i);
     if (__float_as_uint(e) >= tcut) {
       const uint32_t x = philox_x0((uint32_t)i, ctr1, k0, k1);
-      const float u = ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f;  // 2^-24
+      const float u = ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-07f;  // 2^-23, u < 1 exactly
       const float s = e / -logf(u);
       const unsigned long long key = argmax_key(s, (uint32_t)i);
       best = key > best ? key : best;

@@ -33,9 +33,9 @@ def _worker(device: int, inbox, outbox, factory: Callable) -> None:
     try:
         svc = factory(device)
     except BaseException as e:  # report and exit: the pool marks this worker dead
-        outbox.put(("dead", -1, repr(e)))
+        outbox.put(("dead", -1, (device, repr(e))))
         return
-    outbox.put(("ready", -1, None))
+    outbox.put(("ready", -1, (device, None)))
     handles: Dict[int, object] = {}
     lock = threading.Lock()
 
@@ -58,10 +58,14 @@ def _worker(device: int, inbox, outbox, factory: Callable) -> None:
         kind = msg[0]
         if kind == "stop":
             break
-        if kind == "submit":
-            _, rid, text, voice, kw = msg
+        if kind in ("submit", "submit_tokens"):
             try:
-                h = svc.submit(text, voice, **kw)
+                if kind == "submit":
+                    _, rid, text, voice, kw = msg
+                    h = svc.submit(text, voice, **kw)
+                else:  # token-only stream (/v1/completions): chunks are token ids
+                    _, rid, ids, kw = msg
+                    h = svc.submit_tokens(ids, **kw)
             except BaseException as e:
                 outbox.put(("end", rid, repr(e)))
                 continue
@@ -110,8 +114,11 @@ class PoolHandle:
 
 class GpuPool:
     def __init__(self, n_workers: int, factory: Callable = _service_factory,
-                 devices: Optional[List[int]] = None, start_timeout: float = 600.0):
+                 devices: Optional[List[int]] = None, start_timeout: float = 600.0,
+                 poll_s: float = 0.5, respawn: bool = True):
         ctx = mp.get_context("spawn")
+        self.factory, self.poll_s, self.respawn = factory, poll_s, respawn
+        self._respawned: Dict[int, bool] = {}
         self.devices = devices if devices is not None else list(range(n_workers))
         self.inboxes = [ctx.Queue() for _ in self.devices]
         self.outbox = ctx.Queue()
@@ -129,7 +136,7 @@ class GpuPool:
             kind, _, info = self.outbox.get(timeout=start_timeout)
             if kind == "dead":
                 self.close()
-                raise RuntimeError(f"GPU worker failed to start: {info}")
+                raise RuntimeError(f"GPU worker failed to start: {info[1]}")
             ready += 1
         self.alive = [True] * len(self.devices)
         self._reader = threading.Thread(target=self._read, name="mx-pool", daemon=True)
@@ -138,11 +145,19 @@ class GpuPool:
     def _read(self) -> None:
         while True:
             try:
-                kind, rid, payload = self.outbox.get()
+                kind, rid, payload = self.outbox.get(timeout=self.poll_s)
+            except queue.Empty:
+                self._reap()
+                continue
             except (EOFError, OSError):
                 return
             if kind == "closed":
                 return
+            if kind in ("ready", "dead"):  # a replacement worker came up (or failed to)
+                w = self.devices.index(payload[0])
+                with self._lock:
+                    self.alive[w] = kind == "ready"
+                continue
             with self._lock:
                 h = self._handles.get(rid)
                 if kind == "end" and h is not None:
@@ -156,23 +171,63 @@ class GpuPool:
                 h.error = payload
                 h._q.put(None)
 
-    def pick(self) -> int:
-        """Least outstanding tokens; ties to the lowest index."""
-        return min((i for i in range(len(self.load)) if self.alive[i]),
-                   key=lambda i: (self.load[i], i))
+    def _reap(self) -> None:
+        """A worker that died after startup (GPU fault, OOM, signal) ends every stream it
+        held with an error and takes no new ones; a fresh process replaces it (never a
+        re-exec of a process that touched the GPU)."""
+        for w, p in enumerate(self.procs):
+            if not self.alive[w] or p.is_alive():
+                continue
+            with self._lock:
+                self.alive[w] = False
+                lost = [h for h in self._handles.values() if h.worker == w]
+                for h in lost:
+                    self._handles.pop(h.rid, None)
+                self.load[w] = 0
+            for h in lost:
+                h.error = f"GPU worker {w} died (exit code {p.exitcode})"
+                h._q.put(None)
+            if self.respawn and not self._respawned.get(w):  # once per slot: no crash loop
+                self._spawn(w)
 
-    def submit(self, text: str, voice: str = I.DEFAULT_VOICE, max_tokens: Optional[int] = None,
-               **kw) -> PoolHandle:
-        cost = max_tokens or I.MAX_TOKENS
+    def _spawn(self, w: int) -> None:
+        """Start a replacement worker for slot ``w``; it takes requests once ready."""
+        ctx = mp.get_context("spawn")
+        self.inboxes[w] = ctx.Queue()
+        self.procs[w] = ctx.Process(target=_worker, args=(self.devices[w], self.inboxes[w],
+                                                          self.outbox, self.factory), daemon=True)
+        self.procs[w].start()
+        self._respawned[w] = True
+
+    def pick(self) -> int:
+        """Least outstanding tokens over live workers; ties to the lowest index."""
+        live = [i for i in range(len(self.load)) if self.alive[i]]
+        if not live:
+            raise RuntimeError("no GPU worker is alive")
+        return min(live, key=lambda i: (self.load[i], i))
+
+    def _enqueue(self, cost: int, make_msg) -> PoolHandle:
         with self._lock:
             w = self.pick()
             rid = next(self._ids)
             h = PoolHandle(self, rid, w, cost)
             self._handles[rid] = h
             self.load[w] += cost
-        kw = dict(kw, max_tokens=max_tokens)
-        self.inboxes[w].put(("submit", rid, text, voice, kw))
+        self.inboxes[w].put(make_msg(rid))
         return h
+
+    def submit(self, text: str, voice: str = I.DEFAULT_VOICE, max_tokens: Optional[int] = None,
+               **kw) -> PoolHandle:
+        kw = dict(kw, max_tokens=max_tokens)
+        return self._enqueue(max_tokens or I.MAX_TOKENS,
+                             lambda rid: ("submit", rid, text, voice, kw))
+
+    def submit_tokens(self, prompt_ids, max_tokens: Optional[int] = None, **kw) -> PoolHandle:
+        """Token-only stream on the least-loaded GPU (/v1/completions): ``get`` -> id | None."""
+        kw = dict(kw, max_tokens=max_tokens)
+        ids = [int(t) for t in prompt_ids]
+        return self._enqueue(max_tokens or I.MAX_TOKENS,
+                             lambda rid: ("submit_tokens", rid, ids, kw))
 
     def stream(self, text: str, voice: str = I.DEFAULT_VOICE, max_tokens: Optional[int] = None,
                cancel: Optional[threading.Event] = None, **kw) -> Iterator[bytes]:

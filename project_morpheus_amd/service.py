@@ -17,7 +17,6 @@ from __future__ import annotations
 import queue
 import threading
 import warnings
-import zlib
 from typing import Iterator, Optional
 
 import numpy as np
@@ -76,9 +75,10 @@ class Service:
         """Queue one utterance on this GPU's batch loop (non-blocking)."""
         ids = list(prompt_ids) if prompt_ids is not None else self.prompt_ids(text, voice)
         max_tokens = max_tokens or I.MAX_TOKENS
-        # one utterance's random streams (sampling, SNAC noise, synthetic codes) derive from
-        # its content, so its audio does not depend on arrival order or batch company
-        key = zlib.crc32(np.asarray(ids, dtype=np.int32).tobytes()) if seed is None else seed
+        # one utterance's random streams (sampling, SNAC noise, synthetic codes) come from ONE
+        # per-request seed, so its audio never depends on arrival order or batch company;
+        # without a seed it is fresh per request (config.request_seed / CONTENT_SEED)
+        key = C.request_seed(ids, seed)
         req = StreamRequest(
             prompt_ids=ids, max_tokens=max_tokens, penalty=penalty,
             temperature=I.TEMPERATURE if temperature is None else temperature,
@@ -94,7 +94,7 @@ class Service:
                       penalty: float = I.REPETITION_PENALTY, seed: Optional[int] = None):
         """Token-only stream (completions surface): a TokenHandle of generated ids."""
         ids = list(prompt_ids)
-        key = zlib.crc32(np.asarray(ids, dtype=np.int32).tobytes()) if seed is None else seed
+        key = C.request_seed(ids, seed)
         req = StreamRequest(prompt_ids=ids, max_tokens=max_tokens or I.MAX_TOKENS,
                             penalty=penalty,
                             temperature=I.TEMPERATURE if temperature is None else temperature,

@@ -1,4 +1,5 @@
 """Fake per-GPU services for CPU tests of dispatch / adapters (no HIP device needed)."""
+import os
 import queue
 import threading
 import time
@@ -41,10 +42,20 @@ class FakeService:
         self.device = device
 
     def submit(self, text, voice, max_tokens=None, **kw):
+        if text.startswith("die"):  # the worker process dies mid-stream (GPU fault, OOM)
+            threading.Timer(0.3, lambda: os._exit(3)).start()
+            return FakeHandle([b"x"] * 1000, delay=0.01)
         n = max(1, (max_tokens or 70) // 7)
         delay = 0.02 if text.startswith("slow") else 0.0
         fail = "boom" if text.startswith("fail") else None
         return FakeHandle(fake_pcm(text, self.device, n), delay=delay, fail=fail)
+
+
+    def submit_tokens(self, prompt_ids, max_tokens=None, **kw):
+        """Token ids: the prompt ids echoed with the device added, max_tokens of them."""
+        n = max_tokens or 8
+        toks = [(int(prompt_ids[i % len(prompt_ids)]) + self.device) for i in range(n)]
+        return FakeHandle(toks)
 
 
 def fake_factory(device):

@@ -1,0 +1,98 @@
+"""Synthetic Orpheus-shaped weights that SPEAK: greedy decoding emits a designed token script.
+
+Random weights never emit audio ids, so the end-to-end tests used to feed SNAC an injected
+code stream.  These weights close that gap (VERDICT r02 "next round" item 1): the model's own
+greedy tokens run through ``code_of_id`` -> window schedule -> batched SNAC.
+
+Construction (full transformer kept: every layer still computes and perturbs the residual):
+* a *script* is a list of token ids; ``succ(script[i]) = script[i + 1]``, and the prompt's
+  last id maps to ``script[0]``;
+* the embedding row of every id that has a successor is a fresh N(0, 1) vector e_t (rms 1, so
+  the layers' N(0, std) contributions only perturb it);
+* the (untied) lm_head row of ``succ(t)`` is ``GAIN * e_t``: after the final RMSNorm the logit
+  of the successor is ~GAIN * hidden, far above every other logit (random rows N(0, std)).
+
+Scripts exercise the reference schedule's edge cases (speechpipe.py:146-293): a leading text
+id and a mid-stream text id (not custom tokens: skipped), a code-0 id and a special id between
+the custom-token base and the audio base (code <= 0: not accepted, the 7-phase does not
+advance), one out-of-range code (4097: accepted, every window holding it fails the range check,
+so the first window is retried until it passes), then end-of-speech (128258) stops the stream.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from project_morpheus_amd import config as C
+from project_morpheus_amd.weights import synthetic_llm_weights
+
+GAIN = 0.05
+
+
+def speaking_config() -> C.OrpheusConfig:
+    return C.OrpheusConfig(hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024,
+                           vocab=156940, tied=False)
+
+
+def make_script(seed: int, n_accepted: int = 98, text_ids=(2000, 1234),
+                special: int = C.END_OF_HUMAN, invalid_at: int = 9, zero_at: int = 3,
+                special_at: int = 5, avoid: Sequence[int] = ()) -> List[int]:
+    """One utterance's token ids (accepted audio codes in 7-phase order plus the edge cases
+    listed in the module docstring), ending with END_OF_SPEECH."""
+    rng = np.random.default_rng(seed)
+    used = set(int(a) for a in avoid)
+    out: List[int] = []
+
+    def add(t: int) -> None:
+        assert t not in used, t
+        used.add(t)
+        out.append(t)
+
+    add(text_ids[0])
+    for a in range(n_accepted):
+        ph = a % 7  # every audio id below is accepted, so the count equals a
+        if a == zero_at:
+            add(C.AUDIO_CODE_BASE + 4096 * ph + 0)     # code 0: dropped, phase unchanged
+        if a == special_at:
+            add(special)                                # < audio base: code < 0, dropped
+        if a == 40:
+            add(text_ids[1])                            # text id mid-stream: skipped
+        if a == invalid_at:
+            assert ph < 6
+            add(C.AUDIO_CODE_BASE + 4096 * ph + 4097)  # accepted, fails the range check
+            continue
+        while True:
+            t = C.AUDIO_CODE_BASE + 4096 * ph + int(rng.integers(1, 4096))
+            if t not in used:
+                break
+        add(t)
+    out.append(C.END_OF_SPEECH)  # terminal (shared by every script; no successor)
+    return out
+
+
+def speaking_weights(cfg: C.OrpheusConfig, chains: Dict[int, List[int]], seed: int = 91,
+                     std: float = 0.02) -> Dict[str, torch.Tensor]:
+    """``chains``: {start id: script}; greedy decoding after a prompt ending in the start id
+    emits the script.  Scripts must use disjoint ids (one successor per id)."""
+    w = synthetic_llm_weights(cfg, seed=seed, std=std, norm_jitter=0.2)
+    g = torch.Generator().manual_seed(seed + 1)
+    emb = w["embed"].float()
+    head = w["lm_head"].float()
+    succ: Dict[int, int] = {}
+    for start, script in chains.items():
+        prev = start
+        for t in script:
+            assert prev not in succ, f"id {prev} has two successors"
+            succ[prev] = t
+            prev = t
+    for u in set(succ.values()):
+        head[u] = 0.0
+    for t, u in succ.items():  # a shared successor (end-of-speech) sums its predecessors
+        e = torch.randn(cfg.hidden, generator=g)
+        emb[t] = e
+        head[u] += GAIN * e
+    w["embed"] = emb.to(torch.bfloat16)
+    w["lm_head"] = head.to(torch.bfloat16)
+    return w

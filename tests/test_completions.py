@@ -88,3 +88,32 @@ def test_non_streaming_and_errors():
     assert j["choices"][0]["finish_reason"] == "length"
     assert j["usage"]["completion_tokens"] == 2
     assert c.post("/v1/completions", json={"max_tokens": 2}).status_code == 400
+
+
+def test_bad_generation_parameters_are_rejected_before_the_engine():
+    """A request the device cannot run is a 400 for that request, not a loop failure."""
+    seen = []
+    app, _ = _app([CUSTOM_TOKEN_BASE + 11], seen)
+    c = TestClient(app)
+    base = {"prompt": "<|audio|>tara: hi<|eot_id|>", "max_tokens": 2}
+    for bad in ({"top_p": 0.0}, {"top_p": -1}, {"top_p": 1.5}, {"repeat_penalty": 0},
+                {"repeat_penalty": -2.0}, {"temperature": -0.1}, {"temperature": "hot"},
+                {"max_tokens": -3}):
+        r = c.post("/v1/completions", json=dict(base, **bad))
+        assert r.status_code == 400, bad
+    assert seen == []
+    assert c.post("/v1/completions", json=base).status_code == 200
+    import pytest
+    from project_morpheus_amd.batching import check_params
+    with pytest.raises(ValueError):
+        check_params(1.1, float("nan"), 0.9, 10)
+
+
+def test_request_seed_is_fresh_unless_content_seeded(monkeypatch):
+    from project_morpheus_amd import config as C
+    ids = [1, 2, 3]
+    assert C.request_seed(ids, 7) == 7
+    monkeypatch.setattr(C, "CONTENT_SEED", 0)
+    assert len({C.request_seed(ids) for _ in range(8)}) == 8
+    monkeypatch.setattr(C, "CONTENT_SEED", 1)
+    assert C.request_seed(ids) == C.request_seed(list(ids)) != C.request_seed([1, 2, 4])

@@ -55,3 +55,36 @@ def test_worker_error_surfaces(pool):
 def test_stream_generator(pool):
     got = b"".join(pool.stream("xyz", "tara", max_tokens=21))
     assert len(got) == 3 * (128 + 3)
+
+
+def test_submit_tokens_routes_to_a_worker(pool):
+    """/v1/completions on a multi-GPU pool: token streams go through the same dispatch."""
+    h = pool.submit_tokens([5, 6, 7], max_tokens=5)
+    toks = []
+    while True:
+        t = h.get(timeout=30)
+        if t is None:
+            break
+        toks.append(t)
+    assert toks == [5 + h.worker, 6 + h.worker, 7 + h.worker, 5 + h.worker, 6 + h.worker]
+
+
+def test_dead_worker_fails_its_streams_and_is_replaced():
+    p = GpuPool(2, factory=fake_factory, start_timeout=120, poll_s=0.1)
+    try:
+        h = p.submit("die soon", "tara", max_tokens=7000)
+        assert h.worker == 0
+        with pytest.raises(RuntimeError, match="died"):
+            while h.get(timeout=60) is not None:
+                pass
+        assert p.load[0] == 0
+        # the other worker still serves; the replacement for worker 0 comes up
+        assert b"".join(p.stream("abc", "tara", max_tokens=14))
+        deadline = time.time() + 120
+        while not p.alive[0] and time.time() < deadline:
+            time.sleep(0.1)
+        assert p.alive[0]
+        g = p.submit("after", "tara", max_tokens=7)
+        assert list(g.chunks()) == fake_pcm("after", g.worker, 1)
+    finally:
+        p.close()

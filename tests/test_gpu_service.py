@@ -59,10 +59,12 @@ def svc():
     s.test_weights = (w, sw)
     old = service._service
     service._service = s
-    saved = (I.TEMPERATURE, I.MAX_TOKENS)
+    saved = (I.TEMPERATURE, I.MAX_TOKENS, C.CONTENT_SEED)
     I.update_generation_params(temperature=0.0, max_tokens=84)   # greedy: the parity mode
+    C.CONTENT_SEED = 1  # solo and concurrent runs of one text draw the same random streams
     yield s
     I.update_generation_params(temperature=saved[0], max_tokens=saved[1])
+    C.CONTENT_SEED = saved[2]
     service._service = old
     s.close()
 
@@ -163,3 +165,29 @@ def test_reset_frees_row_and_next_request_is_exact(svc):
             assert top2[1] - top2[0] < 1e-2, f"step {k}"
             break
     assert llm is svc.llm
+
+
+def test_bad_request_fails_alone_and_the_loop_serves_on(svc):
+    """ADVICE r02: a request the device rejects (MX_ERR_ARG at prefill) errors by itself;
+    the batch loop keeps serving the next request."""
+    from project_morpheus_amd.batching import StreamRequest, TokenHandle
+    with pytest.raises(ValueError):
+        svc.submit_tokens([1, 2, 3], top_p=0.0)
+    # bypass submit()'s check: the loop itself must isolate the failure
+    req = StreamRequest(prompt_ids=[5, 6, 7], max_tokens=4, top_p=-1.0, audio=False)
+    h = TokenHandle(req)
+    req.on_chunk, req.on_done, req.on_token = h._chunk, h._done, h._token
+    with svc.batch._cv:
+        svc.batch._inbox.append(req)
+        svc.batch._cv.notify()
+    with pytest.raises(ValueError):
+        while h.get(timeout=60) is not None:
+            pass
+    g = svc.submit_tokens([5, 6, 7], max_tokens=6, temperature=0.0)
+    toks = []
+    while True:
+        t = g.get(timeout=60)
+        if t is None:
+            break
+        toks.append(t)
+    assert len(toks) == 6
