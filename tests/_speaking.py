@@ -96,3 +96,20 @@ def speaking_weights(cfg: C.OrpheusConfig, chains: Dict[int, List[int]], seed: i
     w["embed"] = emb.to(torch.bfloat16)
     w["lm_head"] = head.to(torch.bfloat16)
     return w
+
+
+STARTS = [C.START_OF_SPEECH, 3001, 3002, 3003]
+
+
+def four_scripts() -> List[List[int]]:
+    """Four disjoint scripts (one per start id in STARTS) with their edge cases at different
+    places: code-0 ids, specials and out-of-range ids never collide across scripts."""
+    scripts: List[List[int]] = []
+    used: List[int] = list(STARTS)
+    for b in range(4):
+        s = make_script(50 + b, text_ids=(2000 + 10 * b, 1234 + 10 * b),
+                        special=C.END_OF_HUMAN if b == 0 else C.CUSTOM_TOKEN_BASE + 4 + b,
+                        zero_at=3 + b, invalid_at=9 + b, avoid=used)
+        scripts.append(s)
+        used += s[:-1]
+    return scripts

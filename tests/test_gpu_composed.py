@@ -16,7 +16,7 @@ import asyncio
 import numpy as np
 import pytest
 
-from _speaking import make_script, speaking_config, speaking_weights
+from _speaking import STARTS, four_scripts, speaking_config, speaking_weights
 from oracle import llama_ref as L
 from oracle import snac_ref
 from oracle import speechpipe_ref as SP
@@ -27,19 +27,10 @@ from project_morpheus_amd.weights import synthetic_snac_weights
 
 pytestmark = pytest.mark.gpu
 
-STARTS = [C.START_OF_SPEECH, 3001, 3002, 3003]
-
-
 @pytest.fixture(scope="module")
 def world():
     cfg = speaking_config()
-    scripts, used = [], []
-    for b in range(4):
-        s = make_script(50 + b, text_ids=(2000 + 10 * b, 1234 + 10 * b),
-                        special=C.END_OF_HUMAN if b == 0 else C.CUSTOM_TOKEN_BASE + b,
-                        invalid_at=9 + 7 * b, avoid=used + STARTS)
-        scripts.append(s)
-        used += s[:-1]
+    scripts = four_scripts()
     w = speaking_weights(cfg, dict(zip(STARTS, scripts)))
     sw = synthetic_snac_weights(seed=8)  # NoiseBlocks ON: compared with the device noise
     ref = L.LlamaRef(L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,

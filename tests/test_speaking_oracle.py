@@ -4,7 +4,7 @@ with a wide argmax margin at every step, and the script walks the reference sche
 cases (speechpipe.py:146-293) as designed."""
 import numpy as np
 
-from _speaking import make_script, speaking_config, speaking_weights
+from _speaking import STARTS, four_scripts, make_script, speaking_config, speaking_weights
 from oracle import llama_ref as L
 from oracle import speechpipe_ref as SP
 from project_morpheus_amd import config as C
@@ -39,3 +39,17 @@ def test_oracle_greedy_speaks_the_script():
     good = [win for win in wins if SP.codes_valid(*SP.deinterleave(win))]
     assert bad and good
     assert len(good[0]) == 7 and 4097 not in good[0]     # first window after the retries
+
+
+def test_four_disjoint_scripts_share_one_model():
+    """The B = 4 batch test's weights: each start id leads to its own script."""
+    cfg = speaking_config()
+    scripts = four_scripts()
+    w = speaking_weights(cfg, dict(zip(STARTS, scripts)))
+    ref = L.LlamaRef(L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                                 kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab,
+                                 tied=False), w, max_pos=256)
+    for b, start in enumerate(STARTS):
+        prompt = [1001 + b, 1002, start]
+        toks = L.greedy_generate(ref, prompt, len(scripts[b]) + 4, 1.1, stop_ids=C.STOP_IDS)
+        assert toks == scripts[b], b
