@@ -54,13 +54,14 @@ def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512, options=None, info=Non
     return toks, logits
 
 
-def _compare(cfg, w, prompt, steps, penalty=1.1, options=None, info=None):
+def _compare(cfg, w, prompt, steps, penalty=1.1, options=None, info=None, max_pos=512):
     """Teacher-forced comparison: the oracle is fed the GPU's tokens, so every step's
     logits are compared; a token may differ from the oracle's own argmax only where the
     oracle's top-2 margin is below TIE_MARGIN (near-tie).  Returns the number of steps whose
     argmax agreed."""
-    g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, penalty, options=options, info=info)
-    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=512)
+    g_toks, g_logits = _run_gpu(cfg, w, prompt, steps, penalty, options=options, info=info,
+                                max_pos=max_pos)
+    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=max_pos)
     r_toks, r_logits = L.greedy_generate(ref, prompt, steps, penalty, return_logits=True,
                                          forced=g_toks)
     agree = 0
@@ -92,21 +93,34 @@ def test_long_prefill_multi_split_small():
     assert _compare(cfg, w, prompt, 90) >= 60
 
 
-def test_long_context_many_splits_small():
-    """250-token prompt (2 prefill splits of 128) then 150 steps: L reaches 400 -> 4 splits,
-    exercising the in-launch split merge (ticket counter) on every decode step."""
+@pytest.mark.parametrize("step", [1, 0], ids=["one_launch", "per_kernel"])
+def test_long_context_many_splits_small(step):
+    """250-token prompt (2 prefill splits of 128) then 150 steps: L reaches 400 -> 4 splits of
+    the per-kernel path's ticket merge, 4-7 64-position splits of the one-launch step's merge."""
     cfg = _cfgs("small")
     w = synthetic_llm_weights(cfg, seed=13, std=0.05, norm_jitter=0.5)
     prompt = [int(x) for x in np.random.default_rng(4).integers(0, cfg.vocab, 250)]
-    assert _compare(cfg, w, prompt, 150) >= 100
+    assert _compare(cfg, w, prompt, 150, options={"step": step}) >= 100
 
 
-def test_decode_parity_orpheus_width_2_layers():
+def test_one_launch_step_long_context():
+    """One-launch step past 16 attention splits (L up to 1,250 = 20 splits of 64): the
+    last-arriving split merges its partials in chunks of 8 plus the new position."""
+    cfg = _cfgs("small")
+    w = synthetic_llm_weights(cfg, seed=14, std=0.05, norm_jitter=0.5)
+    prompt = [int(x) for x in np.random.default_rng(5).integers(0, cfg.vocab, 240)]
+    assert _compare(cfg, w, prompt, 1010, options={"step": 1}, max_pos=1280) >= 600
+
+
+@pytest.mark.parametrize("step", [1, 0], ids=["one_launch", "per_kernel"])
+def test_decode_parity_orpheus_width_2_layers(step):
+    """B = 1 at Orpheus widths: the one-launch dataflow step (step_kernels.hip, the default)
+    and the per-kernel hipGraph step both follow the oracle."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=0)
     prompt = [128259, 128000] + [int(x) for x in np.random.default_rng(3).integers(1000, 128000, 12)] \
         + [128009, 128260, 128261, 128257]
-    assert _compare(cfg, w, prompt, 24) >= 20
+    assert _compare(cfg, w, prompt, 24, options={"step": step}) >= 20
 
 
 def _orpheus_prompt(n_text, seed):
