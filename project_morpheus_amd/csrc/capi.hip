@@ -283,7 +283,8 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->samp_top_p, slots);
   A(x->samp_seed, 2 * slots);
   A(x->logits, (size_t)c.max_batch * c.vocab);
-  x->step_ok = step_supported(c.hidden, c.ffn, c.heads, c.kv_heads, f8);
+  x->step_ok = step_supported(c.hidden, c.ffn, c.heads, c.kv_heads, f8) &&
+               c.max_pos <= 128 * STEP_SPLIT;
   if (x->step_ok) {
     const int QD = c.heads * 128, KV = c.kv_heads * 128;
     const int grp = c.heads / c.kv_heads;

@@ -228,6 +228,12 @@ __device__ __forceinline__ int* ctr(const StepArgs& a, int l, int slot) {
 // written by earlier launches); q arrives through the hand-off.  The last-arriving split of g
 // merges every split with the new position (q . k_new, v_new) and publishes att[g heads].
 // ---------------------------------------------------------------------------------------
+// LDS floats of an attention block (layout in att_block), for up to STEP_MAX_SPLITS splits
+constexpr int STEP_MAX_SPLITS = 128;
+__host__ __device__ constexpr int att_lds_floats(int grp) {
+  return grp * (128 + 4 * 16 + 8 + 4 * 128) + 260 + STEP_MAX_SPLITS * grp * 2;
+}
+
 template <int GRP>
 __device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* flag) {
   const int QD = a.heads * 128;
@@ -262,6 +268,8 @@ __device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* fl
   float* vn = kn + 128;
   float* sn = vn + 128;              // [GRP]
   float* sml = sn + 4;               // [nsplit][GRP][2]
+  if (s == 0 && tid == 0 && (pos + STEP_SPLIT - 1) / STEP_SPLIT > a.nsplit)
+    atomicCAS(a.status, 0, 9);  // the host sized the grid for fewer positions
   if (wid == 0) wait_for(ctr(a, l, C_QKV + g), 1, (GRP + 2) * 16, a.status, 2);
   __syncthreads();
   const float* qg = a.q + (size_t)l * QD + (size_t)g * GRP * 128;
@@ -406,7 +414,9 @@ __device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* fl
 template <bool F8, int KH, int KF, int GRP>
 __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
   constexpr int EPC = F8 ? 16 : 8;
-  constexpr int XS = (KF > KH ? KF : KH) * 64 * (EPC / 4);  // float4s of the largest stage
+  constexpr int XG = (KF > KH ? KF : KH) * 64 * (EPC / 4);  // float4s of the largest GEMV input
+  constexpr int XA = (att_lds_floats(GRP) + 3) / 4;           // attention scratch
+  constexpr int XS = XG > XA ? XG : XA;
   __shared__ __attribute__((aligned(16))) float4 xs[XS];
   __shared__ float red[4];
   __shared__ int flag;
@@ -586,7 +596,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
       k = o > k ? o : k;
     }
     if (lane == 0) {
-      const int tok = (int)argmax_index(k);
+      const int tok = min((int)argmax_index(k) & 0x7fffffff, a.V - 1);  // (a failed step only)
       tok_s = tok;
       if (a.commit) {
         const int slot = a.row_slot[0];
@@ -651,7 +661,7 @@ bool step_supported(int H, int F, int heads, int kvh, bool f8) {
 
 hipError_t launch_step(const StepArgs& a, bool f8, hipStream_t st) {
   if (a.heads * 128 != a.H || a.kvh > 8 || a.heads % a.kvh || a.nsplit < 1 ||
-      a.nsplit > a.split_max)
+      a.nsplit > a.split_max || a.split_max > step::STEP_MAX_SPLITS)
     return hipErrorInvalidValue;
   const int grp = a.heads / a.kvh;
   const int64_t nb = step_blocks(a);

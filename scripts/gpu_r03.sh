@@ -22,7 +22,7 @@ for v in ${TRACES:-}; do   # e.g. TRACES="bf16 fp8"
   flag=""; [ "$v" = fp8 ] && flag="--fp8"
   step trace_$v 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_$v" -o run -- python3 scripts/trace_step.py $flag ${TRACE_ARGS:-}
   f=$(find "$OUT/trace_$v" -name '*kernel_trace.csv' | head -1)
-  [ -n "$f" ] && python3 scripts/step_gaps.py "$f" 10 > "$OUT/gaps_$v.txt" && cat "$OUT/gaps_$v.txt" | head -20
+  [ -n "$f" ] && python3 scripts/step_gaps.py "$f" 10 ${MARKER:-commit_kernel} > "$OUT/gaps_$v.txt" && cat "$OUT/gaps_$v.txt" | head -20
   find "$OUT/trace_$v" -name '*.csv' -size +5M -delete
 done
 [ "${SKIP_BENCH:-1}" = 1 ] || step bench 900 python bench.py ${BENCH_ARGS:-}
