@@ -173,6 +173,29 @@ def mx_voice_mapper(schema) -> Dict[str, Any]:
     return {"voice": voice if voice in I.AVAILABLE_VOICES else I.DEFAULT_VOICE}
 
 
-def register(registry, name: str = "mi355x") -> None:
+def register(registry, name: str = "mi355x", constructor=None) -> None:
     """``registry.register(name, constructor, describe, voice_mapper)`` (adapter_registry.py:76-83)."""
-    registry.register(name, MxTTSAdapter, mx_describe, mx_voice_mapper)
+    registry.register(name, constructor or MxTTSAdapter, mx_describe, mx_voice_mapper)
+
+
+class AdapterRegistry:
+    """The registry contract the reference server creates adapters through
+    (tts_engine/adapter_registry.py:70-98): ``register``, ``available`` (name -> descriptor)
+    and ``create(name, *, prompt, voice, **kw)`` = ``constructor(prompt=prompt,
+    **voice_mapper(voice), **kw)``.  This build's server keeps one with ``mi355x``; the
+    reference's own registry takes the same adapter through ``register``."""
+
+    def __init__(self) -> None:
+        self._specs: Dict[str, tuple] = {}
+
+    def register(self, name: str, constructor, describe, voice_mapper) -> None:
+        self._specs[name] = (constructor, describe, voice_mapper)
+
+    def available(self) -> Dict[str, Dict[str, Any]]:
+        return {name: spec[1]() for name, spec in self._specs.items()}
+
+    def create(self, name: str, *, prompt: str, voice, **kw):
+        constructor, _, mapper = self._specs[name]
+        params = mapper(voice)
+        params.update(kw)
+        return constructor(prompt=prompt, **params)

@@ -1,11 +1,18 @@
 """The ``/v1/audio/speech`` and ``/ws/tts`` streaming surface over ``MxTTSAdapter``.
 
 Restates the reference routes (Morpheus_Client/server.py:50-87 RIFF header + raw PCM16 frames,
-:161-190 ``SpeechRequest`` / ``create_speech_api``, :209-222 ``tts_ws``) for the MI355X
-adapter, so the HTTP-level path can be served and measured without the reference's control
-plane (orchestrator ladder / playback buffer / text sources are out of scope).
-With the server's stitcher at ``overlap_ms=0`` (server.py:154-156) the reference body is the
-adapter's PCM concatenated, which is what is streamed here.
+:127-158 ``orchestrated_pcm_stream``, :161-190 ``SpeechRequest`` / ``create_speech_api``,
+:209-222 ``tts_ws``, :236-239 ``/adapters``, :243-289 adapter / voice selection by
+``POST /config``) for the MI355X adapter.  As in the reference, BOTH speech routes run the
+orchestrated stream: an ``Orchestrator`` pulling ``ChunkLadder`` byte windows from the adapter,
+the per-pull structured log, ``stitch_chunks`` (overlap 0) and the WAV streamer
+(orchestrator.py).  ``orchestrated=False`` drains the adapter with 4096-byte pulls instead (one
+SNAC window per pull; a bench comparison, not the reference behaviour).  Pinned to the
+reference server's own bytes by tests/test_server_golden.py (golden made by importing
+``Morpheus_Client.server`` with this adapter registered, tests/golden/make_server_golden.py).
+
+Out of scope (control plane): text sources, ``/stats``, barge-in routes, the
+admin UI and ``.env`` persistence of ``/config``.
 
     uvicorn project_morpheus_amd.server:app          # or build_app(adapter_cls=...)
 """
@@ -23,9 +30,9 @@ from starlette.routing import Route, WebSocketRoute
 from starlette.websockets import WebSocket, WebSocketDisconnect
 
 from . import inference as I
-from .adapter import MxTTSAdapter
+from .adapter import AdapterRegistry, MxTTSAdapter, register
 
-PULL_BYTES = 4096  # one reference SNAC window per pull (speechpipe.py:120-135)
+PULL_BYTES = 4096  # one reference SNAC window per pull (speechpipe.py:120-135), unorchestrated
 
 
 def riff_header(sample_rate: int = I.SAMPLE_RATE) -> bytes:
@@ -40,6 +47,16 @@ class SpeechRequest(BaseModel):
     voice: str = I.DEFAULT_VOICE
     response_format: str = "wav"
     speed: float = 1.0
+
+
+class VoiceSchema(BaseModel):
+    """adapter_registry.py:22-36 (only ``voice`` / ``timbre`` are read by the mapper)."""
+    voice: Optional[str] = None
+    timbre: Optional[str] = None
+    prosody: Optional[str] = None
+    accent: Optional[str] = None
+    emotion_priors: Optional[str] = None
+    pace: Optional[str] = None
 
 
 async def adapter_pcm(adapter) -> "AsyncIterator[bytes]":
@@ -57,16 +74,32 @@ def _service_tokens(prompt_ids, **params):
     return get_service().submit_tokens(prompt_ids, **params)
 
 
-def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=None,
-              decode=None, orchestrated: bool = False, orchestrators=None) -> Starlette:
-    """``token_source(prompt_ids, **params)`` backs /v1/completions (default: this GPU's
-    service); ``encode`` / ``decode`` default to the process tokenizer.  ``orchestrated``:
-    /v1/audio/speech runs the reference's Orchestrator contract (ladder pulls of 8-64 bytes,
-    per-pull JSON/base64 log, stitcher; orchestrator.py) instead of 4096-byte pulls."""
+def build_app(adapter_cls=None, token_source=_service_tokens, encode=None,
+              decode=None, orchestrated: bool = True, orchestrators=None,
+              registry: Optional[AdapterRegistry] = None) -> Starlette:
+    """``adapter_cls`` (tests / bench): the class registered as ``mi355x`` (default
+    ``MxTTSAdapter``).  ``token_source(prompt_ids, **params)`` backs /v1/completions (default:
+    this GPU's service); ``encode`` / ``decode`` default to the process tokenizer.
+    ``orchestrators`` collects each request's Orchestrator (pull counts for the bench)."""
     from .completions import build_route
+    from .orchestrator import orchestrated_pcm_stream
     from .tokenizer import default_tokenizer
     if encode is None:
         encode = lambda s: default_tokenizer().encode(s)  # noqa: E731
+    if registry is None:
+        registry = AdapterRegistry()
+        register(registry, constructor=adapter_cls or MxTTSAdapter)
+    state = {"adapter": "mi355x", "voice": VoiceSchema(voice=I.DEFAULT_VOICE)}
+
+    def make_adapter(prompt: str, voice, **kw):
+        schema = state["voice"] if voice is None else VoiceSchema(voice=voice)
+        return registry.create(state["adapter"], prompt=prompt, voice=schema, **kw)
+
+    def pcm_stream(adapter):
+        if orchestrated:
+            return orchestrated_pcm_stream(adapter, orchestrators)
+        return adapter_pcm(adapter)
+
     async def speech(request: Request) -> StreamingResponse:
         try:
             payload = SpeechRequest(**await request.json())
@@ -74,19 +107,14 @@ def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=Non
             raise HTTPException(status_code=400, detail=str(exc)) from exc
         if not payload.input:
             raise HTTPException(status_code=400, detail="Missing input text")
-        adapter = adapter_cls(payload.input, I.resolve_voice(payload.voice),
-                              use_batching=len(payload.input) > 1000, max_batch_chars=1000)
+        adapter = make_adapter(payload.input, payload.voice,
+                               use_batching=len(payload.input) > 1000, max_batch_chars=1000)
 
         async def body():
             done = False
             try:
                 yield riff_header()
-                if orchestrated:
-                    from .orchestrator import orchestrated_pcm_stream
-                    pcm_iter = orchestrated_pcm_stream(adapter, orchestrators)
-                else:
-                    pcm_iter = adapter_pcm(adapter)
-                async for pcm in pcm_iter:
+                async for pcm in pcm_stream(adapter):
                     yield pcm
                 done = True
             finally:
@@ -107,11 +135,10 @@ def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=Non
             if not prompt:
                 await websocket.close(code=1008)
                 return
-            voice = I.resolve_voice(websocket.query_params.get("voice") or I.DEFAULT_VOICE)
-            adapter = adapter_cls(prompt, voice)
+            adapter = make_adapter(prompt, websocket.query_params.get("voice"))
             try:
                 await websocket.send_bytes(riff_header())
-                async for pcm in adapter_pcm(adapter):
+                async for pcm in pcm_stream(adapter):
                     await websocket.send_bytes(pcm)
                 await websocket.close()
             finally:
@@ -119,11 +146,38 @@ def build_app(adapter_cls=MxTTSAdapter, token_source=_service_tokens, encode=Non
         except WebSocketDisconnect:
             pass
 
+    async def adapters(request: Request) -> JSONResponse:
+        return JSONResponse(registry.available())
+
+    async def get_config(request: Request) -> JSONResponse:
+        return JSONResponse({"adapter": state["adapter"], "voice": state["voice"].voice})
+
+    async def update_config(request: Request) -> JSONResponse:
+        """server.py:243-289, the adapter / voice part (no .env persistence)."""
+        try:
+            data = await request.json()
+        except Exception as exc:
+            raise HTTPException(status_code=400, detail=str(exc)) from exc
+        name = data.get("adapter")
+        if name:
+            if name not in registry.available():
+                raise HTTPException(status_code=404, detail="Unknown adapter")
+            state["adapter"] = name
+        voice = data.get("voice")
+        if voice:
+            state["voice"] = VoiceSchema(**voice) if isinstance(voice, dict) \
+                else VoiceSchema(voice=voice)
+        return JSONResponse({"message": "ok", "adapter": state["adapter"],
+                             "voice": state["voice"].model_dump()})
+
     return Starlette(routes=[Route("/v1/audio/speech", speech, methods=["POST"]),
                              Route("/v1/completions", build_route(token_source, encode, decode),
                                    methods=["POST"]),
                              Route("/v1/audio/voices", voices, methods=["GET"]),
-                             WebSocketRoute("/ws/tts", tts_ws)])
+                             WebSocketRoute("/ws/tts", tts_ws),
+                             Route("/adapters", adapters, methods=["GET"]),
+                             Route("/config", get_config, methods=["GET"]),
+                             Route("/config", update_config, methods=["POST"])])
 
 
 app: Optional[Starlette] = build_app()
