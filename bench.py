@@ -171,13 +171,55 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
             "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
 
 
-def run_http(args, syn, prompt_text, inject, local, orchestrated=False):
-    """configs[1] at the HTTP level: one ``POST /v1/audio/speech`` through the ASGI app of
-    ``project_morpheus_amd.server`` (no sockets; the app's own adapter and streaming body),
-    the adapter's source bound to this process's engine.  RTF = audio / wall from request
-    start to the last body chunk; first audio = first non-empty PCM chunk after the header."""
+async def _asgi_speech(app, text: str):
+    """One ``POST /v1/audio/speech`` through an ASGI app (no sockets): (t0, [(t, nbytes)])."""
     import asyncio
     import json as _json
+    body = _json.dumps({"input": text, "voice": "tara"}).encode()
+    sent = {"done": False}
+    marks = []
+
+    async def receive():
+        if not sent["done"]:
+            sent["done"] = True
+            return {"type": "http.request", "body": body, "more_body": False}
+        await asyncio.sleep(3600)
+        return {"type": "http.disconnect"}
+
+    async def send(msg):
+        if msg["type"] == "http.response.body":
+            marks.append((time.perf_counter(), len(msg.get("body", b""))))
+
+    scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1",
+             "method": "POST", "scheme": "http", "path": "/v1/audio/speech",
+             "raw_path": b"/v1/audio/speech", "query_string": b"", "root_path": "",
+             "headers": [(b"content-type", b"application/json")],
+             "client": ("127.0.0.1", 1), "server": ("127.0.0.1", 80)}
+    t0 = time.perf_counter()
+    await app(scope, receive, send)
+    return t0, marks
+
+
+def _http_result(workload, t0, marks, orchs=None):
+    pcm = sum(n for _, n in marks) - 44
+    wall = marks[-1][0] - t0
+    first_pcm = next((t for t, n in marks[1:] if n > 0), t0)
+    out = {"workload": workload, "value": round(pcm / 2 / 24000.0 / wall, 3),
+           "unit": "audio-sec/wall-sec", "first_audio_ms": round(1e3 * (first_pcm - t0), 2),
+           "bytes": pcm}
+    if orchs:
+        out["pulls"] = orchs[-1].pulls
+        out["mean_pull_bytes"] = round(pcm / max(1, orchs[-1].pulls), 2)
+        out["pulls_per_s"] = round(orchs[-1].pulls / wall, 1)
+    return out
+
+
+def run_http(args, syn, prompt_text, inject, local, orchestrated=False):
+    """configs[1] at the HTTP level: one ``POST /v1/audio/speech`` through the ASGI app of
+    ``project_morpheus_amd.server`` (no sockets), the adapter's source bound to this
+    process's ``Synthesizer``.  RTF = audio / wall from request start to the last body chunk;
+    first audio = first non-empty PCM chunk after the header."""
+    import asyncio
 
     import torch
 
@@ -199,48 +241,73 @@ def run_http(args, syn, prompt_text, inject, local, orchestrated=False):
 
     orchs = []
     app = build_app(adapter_cls=BenchAdapter, orchestrated=orchestrated, orchestrators=orchs)
-
-    async def one():
-        body = _json.dumps({"input": prompt_text, "voice": "tara"}).encode()
-        sent = {"done": False}
-        marks = []
-
-        async def receive():
-            if not sent["done"]:
-                sent["done"] = True
-                return {"type": "http.request", "body": body, "more_body": False}
-            await asyncio.sleep(3600)
-            return {"type": "http.disconnect"}
-
-        async def send(msg):
-            if msg["type"] == "http.response.body":
-                marks.append((time.perf_counter(), len(msg.get("body", b""))))
-
-        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1",
-                 "method": "POST", "scheme": "http", "path": "/v1/audio/speech",
-                 "raw_path": b"/v1/audio/speech", "query_string": b"", "root_path": "",
-                 "headers": [(b"content-type", b"application/json")],
-                 "client": ("127.0.0.1", 1), "server": ("127.0.0.1", 80)}
-        t0 = time.perf_counter()
-        await app(scope, receive, send)
-        return t0, marks
-
-    asyncio.run(one())  # warm
-    t0, marks = asyncio.run(one())
-    pcm = sum(n for _, n in marks) - 44
-    first = next(t for t, n in marks[1:] if n > 0) if len(marks) > 1 else t0
-    wall = marks[-1][0] - t0
-    first_pcm = next((t for t, n in marks[1:] if n > 0), t0)
-    out = {"workload": ("configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream)"
+    asyncio.run(_asgi_speech(app, prompt_text))  # warm
+    t0, marks = asyncio.run(_asgi_speech(app, prompt_text))
+    return _http_result("configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream), "
+                        "engine.Synthesizer source"
                         + (", reference Orchestrator contract: ChunkLadder byte pulls (8-64), "
                            "per-pull JSON/base64 log, stitch_chunks, WAV streamer"
-                           if orchestrated else ", 4096-byte pulls")),
-           "value": round(pcm / 2 / 24000.0 / wall, 3), "unit": "audio-sec/wall-sec",
-           "first_audio_ms": round(1e3 * (first_pcm - t0), 2), "bytes": pcm}
-    if orchestrated and orchs:
-        out["pulls"] = orchs[-1].pulls
-        out["mean_pull_bytes"] = round(pcm / max(1, orchs[-1].pulls), 2)
-    return out
+                           if orchestrated else ", 4096-byte pulls"), t0, marks, orchs)
+
+
+def run_http_service(args, llm, snac, cfg, prompt_text):
+    """configs[1] through the SHIPPED serving path: ``POST /v1/audio/speech`` -> default
+    ``MxTTSAdapter`` source -> ``service.Service`` -> ``BatchSynthesizer`` (continuous batching
+    loop, one live stream) on this process's engines, orchestrated byte pulls as the
+    reference server (server.py:127-158)."""
+    import asyncio
+
+    from project_morpheus_amd import inference as I
+    from project_morpheus_amd import service as S
+    from project_morpheus_amd.server import build_app
+    from project_morpheus_amd.tokenizer import Tokenizer
+    saved = (I.TEMPERATURE, I.MAX_TOKENS)
+    I.update_generation_params(temperature=0.0, max_tokens=args.max_tokens)  # greedy
+    svc = S.Service.from_engines(llm, snac, cfg, synthetic_audio=True, tokenizer=Tokenizer(None))
+    old, S._service = S._service, svc
+    try:
+        orchs = []
+        app = build_app(orchestrators=orchs)
+        asyncio.run(_asgi_speech(app, prompt_text))  # warm (graphs, step kernel)
+        t0, marks = asyncio.run(_asgi_speech(app, prompt_text))
+    finally:
+        S._service = old
+        svc.close()
+        I.update_generation_params(temperature=saved[0], max_tokens=saved[1])
+    return _http_result("configs[1] via POST /v1/audio/speech -> default MxTTSAdapter -> "
+                        "Service -> BatchSynthesizer (shipped path), reference Orchestrator "
+                        "byte pulls", t0, marks, orchs)
+
+
+def run_orchestrator_ceiling(audio_seconds: float, unit: str):
+    """Host ceiling of the orchestrated HTTP path alone: the adapter's source yields an
+    already-synthesised utterance (PCM in memory, 4096-byte windows) at once, so the RTF is
+    what the Orchestrator's ladder pulls + base64 JSON log + stitcher + WAV streamer sustain
+    (reference orchestrator/core.py:89-117) with ``pull_unit`` = bytes (the reference
+    contract) or ms (the descriptor's unit, config.PULL_UNIT)."""
+    import asyncio
+
+    from project_morpheus_amd.adapter import MxTTSAdapter
+    from project_morpheus_amd.server import build_app
+    n = int(audio_seconds * 24000) * 2
+    pcm = (bytes(range(256)) * (n // 256 + 1))[:n]
+
+    class Prefilled(MxTTSAdapter):
+        def __init__(self, *a, **k):
+            super().__init__(*a, pull_unit=unit, **k)
+
+        @staticmethod
+        def source(prompt, voice, use_batching, max_batch_chars, cancel):
+            for i in range(0, len(pcm), 4096):
+                yield pcm[i:i + 4096]
+
+    orchs = []
+    app = build_app(adapter_cls=Prefilled, orchestrators=orchs)
+    asyncio.run(_asgi_speech(app, "Hello world"))
+    t0, marks = asyncio.run(_asgi_speech(app, "Hello world"))
+    return _http_result(f"orchestrated HTTP path with a pre-filled source ({audio_seconds:.1f} s "
+                        f"of PCM in memory), pull unit {unit}: the host ceiling, no GPU",
+                        t0, marks, orchs)
 
 
 def run_long_read(args, llm, snac, rank, world, dist):
@@ -401,10 +468,13 @@ def main():
         firsts = [x for r in fl for x in r]
 
     # ---- configs[1] at the HTTP level (rank 0 only: one request through the ASGI app) ----
-    http_level = http_orch = None
+    http_level = http_orch = http_service = ceiling = None
     if rank == 0 and not args.no_http:
         http_level = run_http(args, syn, "Hello world", inject, local)
         http_orch = run_http(args, syn, "Hello world", inject, local, orchestrated=True)
+        http_service = run_http_service(args, llm, snac, cfg, "Hello world")
+        utt_s = audio / max(1, args.steps) / max(1, world)
+        ceiling = {u: run_orchestrator_ceiling(utt_s, u) for u in ("bytes", "ms")}
 
     # ---- configs[2]: B concurrent streams per GPU, continuous batching + batched SNAC ----
     batched = None
@@ -477,6 +547,8 @@ def main():
             "audio_seconds": round(audio, 3),
             "http_level": http_level,
             "http_level_orchestrator": http_orch,
+            "http_level_service": http_service,
+            "orchestrator_ceiling": ceiling,
             "configs_2_batched": batched,
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,

@@ -63,11 +63,20 @@ class MxTTSAdapter:
     source: Callable[..., Iterator[bytes]] = staticmethod(_default_source)
 
     def __init__(self, prompt: str, voice: str = I.DEFAULT_VOICE, *, use_batching: bool = False,
-                 max_batch_chars: int = 1000) -> None:
+                 max_batch_chars: int = 1000, pull_unit: Optional[str] = None) -> None:
+        """``pull_unit``: "bytes" (the reference contract, default) or "ms" (the unit the
+        descriptor declares: ``pull(n)`` returns n ms of PCM); default from
+        ``config.PULL_UNIT`` (MORPHEUS_MX_PULL_UNIT)."""
+        from .config import PULL_UNIT
         self.prompt = prompt
         self.voice = voice
         self.use_batching = use_batching
         self.max_batch_chars = max_batch_chars
+        unit = pull_unit or PULL_UNIT
+        if unit not in ("bytes", "ms"):
+            raise ValueError(f"pull_unit must be 'bytes' or 'ms', got {unit!r}")
+        # bytes per pull unit: 1, or 24 kHz x 2 bytes / 1000 = 48 per millisecond
+        self._unit_bytes = 1 if unit == "bytes" else 2 * I.SAMPLE_RATE // 1000
         self._buffer = bytearray()
         self._exhausted = False
         self._q: Optional[queue.Queue] = None
@@ -118,6 +127,7 @@ class MxTTSAdapter:
             self._buffer.extend(item)
 
     async def pull(self, chunk_size: int) -> AudioChunk:
+        chunk_size *= self._unit_bytes
         self._start()
         q = self._q
         while len(self._buffer) < chunk_size and not self._exhausted:

@@ -126,6 +126,10 @@ SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
 # "regenerate" gives new audio; 1 derives it from the prompt ids (reproducible bench / parity
 # runs: the same text gives the same audio whatever the batch company or arrival order).
 CONTENT_SEED = env_int("MORPHEUS_MX_CONTENT_SEED", 0)
+# Unit of MxTTSAdapter.pull(n): "bytes" (default; the reference adapters slice bytes,
+# llama_local.py:131-150, pinned by tests/test_tts_adapter_chunking.py) or "ms" (what the
+# adapter descriptor declares, adapter_registry.py:54: n milliseconds of PCM = 48 n bytes).
+PULL_UNIT = os.environ.get("MORPHEUS_MX_PULL_UNIT", "bytes")
 
 
 def request_seed(prompt_ids, seed=None) -> int:

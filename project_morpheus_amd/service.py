@@ -61,6 +61,19 @@ class Service:
         self.batch = BatchSynthesizer(self.llm, self.snac).start()
         self.tok = tokenizer or default_tokenizer()
 
+    @classmethod
+    def from_engines(cls, llm: LlmEngine, snac: SnacDecoder, cfg: C.OrpheusConfig,
+                     synthetic_audio: bool, tokenizer: Optional[Tokenizer] = None) -> "Service":
+        """A service over engines that already exist (bench: the configs[1] line through the
+        shipped adapter -> Service -> BatchSynthesizer path, on the bench's own weights)."""
+        self = cls.__new__(cls)
+        self.cfg, self.device = cfg, llm.device
+        self.synthetic_audio = synthetic_audio
+        self.llm, self.snac = llm, snac
+        self.batch = BatchSynthesizer(llm, snac).start()
+        self.tok = tokenizer or default_tokenizer()
+        return self
+
     @property
     def outstanding_tokens(self) -> int:
         return self.batch.outstanding_tokens

@@ -76,3 +76,21 @@ def test_orchestrated_speech_route():
     assert r.status_code == 200
     assert r.content == riff_header() + b"".join(PCM)
     assert orchs and orchs[0].pulls >= len(b"".join(PCM)) // 64
+
+
+def test_ms_pull_unit_option():
+    """MORPHEUS_MX_PULL_UNIT=ms / pull_unit="ms": pull(n) returns n ms of PCM (48 n bytes),
+    what the adapter descriptor declares (adapter_registry.py:54); default stays bytes."""
+    async def go(unit):
+        a = Fake("x", pull_unit=unit)
+        o = Orchestrator(a, PlaybackBuffer(1000))
+        out = [c async for c in o.stream()]
+        return o.pulls, b"".join(c.pcm for c in out), [len(c.pcm) for c in out]
+
+    n_b, pcm_b, _ = asyncio.run(go("bytes"))
+    n_ms, pcm_ms, sizes = asyncio.run(go("ms"))
+    assert pcm_b == pcm_ms == b"".join(PCM)
+    assert sizes[0] == 8 * 48 and n_ms < n_b / 10
+    import pytest
+    with pytest.raises(ValueError):
+        Fake("x", pull_unit="frames")
