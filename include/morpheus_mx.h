@@ -118,6 +118,12 @@ int mx_llm_bench_attention(mx_llm* ctx, int L, int n_rows, int cpw, int debug, i
                            float* us_out);
 /* Park decode row `row` on the scratch slot (stream ended / barge-in reset). */
 int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
+/* Row compaction (stream-ordered on `stream`, between steps): the stream bound to row `src`
+ * continues in the parked row `dst` -- same KV slot, position, token and next input; `src`
+ * is parked.  Lets a step run the row class of the live stream count instead of the highest
+ * row index in use (replaces nothing in the reference: vLLM's scheduler compacts its batch
+ * internally, engine_class.py:114-134).  MX_ERR_STATE if `dst` is live. */
+int mx_llm_move_row(mx_llm* ctx, int dst, int src, void* stream);
 /* Host view of decode row `row`: *active = 1 while a stream is bound to it (prefill until
  * release), *next_pos = the position its next token takes. */
 int mx_llm_row_state(const mx_llm* ctx, int row, int* active, int* next_pos);

@@ -69,6 +69,7 @@ _SIGS = {
     "mx_llm_bench_attention": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.POINTER(C.c_float)]),
     "mx_llm_release_row": (C.c_int, [_P, C.c_int, _P]),
+    "mx_llm_move_row": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "mx_llm_row_state": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mx_llm_history": (C.POINTER(C.c_int32), [_P]),
     "mx_llm_debug_logits": (C.c_int, [_P, C.c_int]),

@@ -6,10 +6,13 @@ engine, one request per thread (Orpheus-TTS/orpheus_tts_pypi/orpheus_tts/engine_
 114-134), and decodes each stream's SNAC windows independently (speechpipe.py:191-293).
 ``BatchSynthesizer`` is that loop for the MI355X engine:
 
-* every stream owns one KV slot and one decode row; a step decodes all rows at once
-  (``mx_llm_decode(n_rows)``, one hipGraph per row count), rows without a stream are parked
-  on the scratch slot; each row decodes under its own generation parameters (penalty,
-  temperature, top-p, seed: per-slot state set at prefill);
+* every stream owns one KV slot and one decode row; a step decodes rows [0, n_rows) at once
+  (``mx_llm_decode(n_rows)``: one hipGraph per row count, the one-launch step for one row),
+  rows without a stream are parked on the scratch slot; each row decodes under its own
+  generation parameters (penalty, temperature, top-p, seed: per-slot state set at prefill);
+* rows are compacted: when a stream ends, the highest live row moves into the lowest free
+  one (``mx_llm_move_row``: same KV slot, stream-ordered between steps), so a step runs the
+  row class of the live stream count, not of the highest row index ever used;
 * a stream is admitted as soon as it has arrived and a row is free: its prefill is enqueued
   between steps (ordered on the same HIP stream, nothing drains);
 * ``depth`` steps stay queued on the GPU; tokens are read from the host-mapped history when
@@ -113,8 +116,12 @@ def check_params(penalty: float, temperature: float, top_p: float, max_tokens: i
 
 
 class _Row:
+    """One stream's decode state; ``idx`` is the device row it decodes in (rows are compacted,
+    so it can change), ``slot`` its KV slot (fixed for the stream's life)."""
+
     def __init__(self, idx: int):
         self.idx = idx
+        self.slot = -1
         self.req: Optional[StreamRequest] = None
         self.sched: Optional[WindowScheduler] = None
         self.n0 = 0          # prompt length (position of generated token 0)
@@ -191,10 +198,12 @@ class TokenHandle(StreamHandle):
 
 class BatchSynthesizer:
     def __init__(self, llm: LlmEngine, snac: SnacDecoder, depth: Optional[int] = None, seed: int = 0,
-                 snac_min_batch: Optional[int] = None, snac_max_hold: Optional[int] = None):
+                 snac_min_batch: Optional[int] = None, snac_max_hold: Optional[int] = None,
+                 compact: bool = True):
         if llm.max_slots < llm.max_batch:
             raise ValueError("BatchSynthesizer needs one KV slot per decode row")
         self.llm, self.snac, self.seed = llm, snac, seed
+        self.compact = compact  # row compaction (mx_llm_move_row) when streams end
         self.depth = max(1, BATCH_DEPTH if depth is None else depth)
         # SNAC window coalescing: due windows are held until `snac_min_batch` of them are
         # ready or the oldest has waited `snac_max_hold` decode steps (a stream's first window
@@ -313,6 +322,7 @@ class BatchSynthesizer:
     def _loop(self, t0: float, poll, idle, finished, done_cb) -> None:
         llm, B = self.llm, self.llm.max_batch
         rows = [_Row(i) for i in range(B)]
+        free_slots = set(range(llm.max_slots))
         waiting: Deque[StreamRequest] = deque()
         inflight: Deque = deque()   # (event, [(row, req, k)])
         pending: Deque = deque()    # (event, ring index, [(req, nbytes)])
@@ -356,9 +366,10 @@ class BatchSynthesizer:
                 if req.noise_seed is None:
                     req.noise_seed = (self.seed * 1000003 + self._admitted) & _MASK48
                 self._admitted += 1
+                slot = min(free_slots)
                 try:  # a request the device rejects fails alone; the loop serves on
                     check_params(req.penalty, req.temperature, req.top_p, req.max_tokens)
-                    llm.prefill(r.idx, r.idx, req.prompt_ids, req.penalty, self.stream,
+                    llm.prefill(slot, r.idx, req.prompt_ids, req.penalty, self.stream,
                                 temperature=req.temperature, top_p=req.top_p, seed=req.seed)
                 except (ValueError, _lib.MxError) as e:
                     if isinstance(e, _lib.MxError) and e.rc != _lib.MX_ERR_ARG:
@@ -366,6 +377,8 @@ class BatchSynthesizer:
                     req.error = e
                     complete(req)
                     continue
+                free_slots.discard(slot)
+                r.slot = slot
                 r.req, r.sched, r.n0 = req, WindowScheduler(), n0
                 r.limit = max(1, min(req.max_tokens, llm.max_pos - n0))
                 r.issued, r.stopped, r.parked = 1, False, False
@@ -431,7 +444,27 @@ class BatchSynthesizer:
                     req.windows += 1
             park(r)
             closing.append(req)
-            r.req, r.sched, r.stopped, r.parked = None, None, False, False
+            free_slots.add(r.slot)
+            r.req, r.sched, r.stopped, r.parked, r.slot = None, None, False, False, -1
+
+        def compact():
+            """Move the highest live row into the lowest free one, so a step runs the row
+            class of the live stream count (a lone stream in row 31 no longer costs a 32-row
+            step; a single stream decodes in row 0 on the one-launch step)."""
+            if not self.compact:
+                return
+            while True:
+                free = [r for r in rows if r.req is None]
+                live = [r for r in rows if r.req is not None and not r.stopped and not r.parked]
+                if not free or not live:
+                    return
+                lo, hi = free[0], live[-1]
+                if lo.idx > hi.idx:
+                    return
+                llm.move_row(lo.idx, hi.idx, self.stream)
+                i, j = lo.idx, hi.idx
+                rows[i], rows[j] = hi, lo
+                hi.idx, lo.idx = i, j
 
         def announce():
             # a closing stream's windows were all launched when it closed: once no pending
@@ -449,6 +482,7 @@ class BatchSynthesizer:
                 if r.req is not None and r.req.cancelled:
                     finish(r, [])
             admit()
+            compact()
             act = [r for r in rows if r.req is not None and not r.stopped and not r.parked]
             # keep `depth` steps queued for the rows that still need tokens
             while act and len(inflight) < self.depth:
@@ -479,7 +513,7 @@ class BatchSynthesizer:
             for r, req, k in entries:
                 if r.req is not req or r.stopped or req.cancelled:
                     continue  # speculative step of a stream that already ended
-                tok = int(llm.hist[r.idx, r.n0 + k])
+                tok = int(llm.hist[r.slot, r.n0 + k])
                 req.tokens.append(tok)
                 if req.on_token is not None:
                     req.on_token(req, tok)

@@ -1135,6 +1135,22 @@ extern "C" int mx_llm_release_row(mx_llm* x, int row, void* stream) {
   return MX_OK;
 }
 
+extern "C" int mx_llm_move_row(mx_llm* x, int dst, int src, void* stream) {
+  if (!x || dst < 0 || src < 0 || dst >= x->c.max_batch || src >= x->c.max_batch || dst == src)
+    return MX_ERR_ARG;
+  if (x->row_active[dst]) MX_FAIL(x, MX_ERR_STATE, "move_row: destination row is live");
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, launch_move_row(x->row_slot, x->row_pos, x->row_token, x->h_dec, x->c.hidden, dst,
+                            src, x->c.max_slots, (hipStream_t)stream));
+  x->pos_mirror[dst] = x->pos_mirror[src];
+  x->row_active[dst] = x->row_active[src];
+  x->row_samples[dst] = x->row_samples[src];
+  x->pos_mirror[src] = 0;
+  x->row_active[src] = 0;
+  x->row_samples[src] = 0;
+  return MX_OK;
+}
+
 extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next_pos) {
   if (!x || !active || !next_pos || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
   *active = x->row_active[row];

@@ -857,6 +857,29 @@ __global__ void scatter_rows_kernel(void* dst, const void* src, const int32_t* d
   }
 }
 
+// Row compaction: the stream decoded by row `src` continues in row `dst` (its KV slot, position,
+// current token and next input embedding move; `src` is parked on the scratch slot).
+__global__ void move_row_kernel(int32_t* slot, int32_t* pos, int32_t* token, float* h, int hidden,
+                                int dst, int src, int scratch) {
+  const float4* s4 = reinterpret_cast<const float4*>(h + (size_t)src * hidden);
+  float4* d4 = reinterpret_cast<float4*>(h + (size_t)dst * hidden);
+  for (int c = threadIdx.x; c < (hidden >> 2); c += blockDim.x) d4[c] = s4[c];
+  if (threadIdx.x == 0) {
+    slot[dst] = slot[src];
+    pos[dst] = pos[src];
+    token[dst] = token[src];
+    slot[src] = scratch;
+    pos[src] = 0;
+  }
+}
+
+hipError_t launch_move_row(int32_t* slot, int32_t* pos, int32_t* token, float* h, int hidden,
+                           int dst, int src, int scratch, hipStream_t st) {
+  hipLaunchKernelGGL(move_row_kernel, dim3(1), dim3(256), 0, st, slot, pos, token, h, hidden, dst,
+                     src, scratch);
+  return hipGetLastError();
+}
+
 // rows [0,n): slot[i] = slot_val, pos[i] = pos0 + i
 __global__ void set_rows_kernel(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -119,6 +119,8 @@ hipError_t launch_set_slot_params(float* penalty, float* temp, float* top_p, uin
 hipError_t launch_set_rows(int32_t* slot, int32_t* pos, int n, int slot_val, int pos0,
                            hipStream_t st);
 hipError_t launch_set_scalar(float* p, float v, hipStream_t st);
+hipError_t launch_move_row(int32_t* slot, int32_t* pos, int32_t* token, float* h, int hidden,
+                           int dst, int src, int scratch, hipStream_t st);
 hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st);
 hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t* embed,

@@ -144,6 +144,10 @@ class LlmEngine:
     def release_row(self, row: int, stream) -> None:
         self._check(self.lib.mx_llm_release_row(self.h, row, C.c_void_p(stream.cuda_stream)))
 
+    def move_row(self, dst: int, src: int, stream) -> None:
+        """Compaction: row ``src``'s stream continues in parked row ``dst`` (same KV slot)."""
+        self._check(self.lib.mx_llm_move_row(self.h, dst, src, C.c_void_p(stream.cuda_stream)))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.mx_llm_destroy(self.h)
