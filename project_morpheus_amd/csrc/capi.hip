@@ -150,6 +150,8 @@ struct mx_llm {
   int* st_status_host = nullptr;  // host-mapped copy (finish block)
   int* st_status_dev = nullptr;
   unsigned long long* st_best = nullptr;
+  unsigned long long* st_trace = nullptr;  // option step_trace: per-block timeline (diagnostic)
+  int64_t st_trace_blocks = 0, st_last_blocks = 0;
 
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -850,6 +852,8 @@ static hipError_t enqueue_step(mx_llm* x, hipStream_t st) {
   a.nsplit = std::max(1, (pos + STEP_SPLIT - 1) / STEP_SPLIT);
   const bool sample = x->row_samples[0] != 0;
   a.commit = sample ? 0 : 1;
+  a.trace = x->st_trace;
+  x->st_last_blocks = step_blocks(a);
   hipError_t e = launch_step(a, c.wdtype == WT_FP8, st);
   if (e != hipSuccess || !sample) return e;
   SampleArgs sa{};
@@ -1077,6 +1081,18 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "step") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "step must be 0 or 1");
     x->step = value;
+  } else if (k == "step_trace") {  // diagnostic: per-block timeline of one-launch steps
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "step_trace must be 0 or 1");
+    if (value && !x->st_trace && x->step_ok) {
+      StepArgs g{};
+      g.H = x->c.hidden; g.F = x->c.ffn; g.heads = x->c.heads; g.kvh = x->c.kv_heads;
+      g.V = x->c.vocab; g.layers = x->c.layers; g.nsplit = x->step_split_max;
+      x->st_trace_blocks = step_blocks(g);
+      MX_TRY(x, hipSetDevice(x->device));
+      MX_TRY(x, x->alloc(&x->st_trace, (size_t)x->st_trace_blocks * 4));
+      MX_TRY(x, hipMemset(x->st_trace, 0, (size_t)x->st_trace_blocks * 32));
+    }
+    if (!value) x->st_trace = nullptr;  // (the buffer stays allocated until destroy)
   } else if (k == "rows_frag") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
     x->rows_frag = value;
@@ -1149,6 +1165,17 @@ extern "C" int mx_llm_move_row(mx_llm* x, int dst, int src, void* stream) {
   x->row_active[src] = 0;
   x->row_samples[src] = 0;
   return MX_OK;
+}
+
+// Diagnostic: copy the last one-launch step's per-block timeline (4 u64 per block: entry,
+// wait done, end on the 100 MHz constant clock, role << 32 | layer) after syncing `stream`.
+extern "C" int64_t mx_llm_step_trace(mx_llm* x, unsigned long long* host, int64_t max_blocks,
+                                     void* stream) {
+  if (!x || !host || !x->st_trace) return -1;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
+  const int64_t n = std::min(max_blocks, x->st_last_blocks);
+  if (hipMemcpy(host, x->st_trace, (size_t)n * 32, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
 }
 
 extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next_pos) {

@@ -43,6 +43,7 @@ struct StepArgs {
   int H, F, heads, kvh, V, layers, max_pos, nsplit, split_max, scratch_slot;
   float eps, att_scale;
   int commit;                                // 1: finish commits the argmax (greedy row)
+  unsigned long long* trace;                 // diagnostic: [blocks][4] timestamps (null: off)
 };
 
 // Blocks of the launch: layers * (qkv + attention + o + gate/up + down) + lm_head + 1.

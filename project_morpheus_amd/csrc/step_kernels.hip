@@ -235,7 +235,8 @@ __host__ __device__ constexpr int att_lds_floats(int grp) {
 }
 
 template <int GRP>
-__device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* flag) {
+__device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* flag,
+                          unsigned long long* tw) {
   const int QD = a.heads * 128;
   const int g = idx / a.nsplit, s = idx - g * a.nsplit;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -272,6 +273,7 @@ __device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* fl
     atomicCAS(a.status, 0, 9);  // the host sized the grid for fewer positions
   if (wid == 0) wait_for(ctr(a, l, C_QKV + g), 1, (GRP + 2) * 16, a.status, 2);
   __syncthreads();
+  if (a.trace && tid == 0) *tw = __builtin_amdgcn_s_memrealtime();
   const float* qg = a.q + (size_t)l * QD + (size_t)g * GRP * 128;
   if (tid < GRP * 32) {
     const float4 v = ld4_wt(qg, (size_t)tid * 4);
@@ -421,7 +423,21 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
   __shared__ float red[4];
   __shared__ int flag;
   __shared__ unsigned long long bkey[4];
+  __shared__ unsigned long long t_w;  // diagnostic trace: when the block's wait ended
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const unsigned long long t_e = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // diagnostic trace (a.trace != null only): per block {entry, wait done, end, role << 32 |
+  // layer} on the 100 MHz constant clock
+#define STEP_WAITED() \
+  if (a.trace && tid == 0) t_w = __builtin_amdgcn_s_memrealtime();
+#define STEP_DONE(role_, layer_)                                                    \
+  if (a.trace && tid == 0) {                                                        \
+    unsigned long long* tr_ = a.trace + (size_t)b * 4;                              \
+    tr_[0] = t_e;                                                                   \
+    tr_[1] = t_w;                                                                   \
+    tr_[2] = __builtin_amdgcn_s_memrealtime();                                      \
+    tr_[3] = ((unsigned long long)(role_) << 32) | (unsigned)(layer_);              \
+  }
   const Geo G(a);
   const int64_t b = blockIdx.x;
   const int H = a.H, QD = a.heads * 128;
@@ -443,6 +459,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
       const float cs = a.rope_cos[(size_t)pos * 64 + pr], sn = a.rope_sin[(size_t)pos * 64 + pr];
       if (l > 0 && wid == 0) wait_for(ctr(a, l - 1, C_DN), 8, G.ND, a.status, 1);
       __syncthreads();
+      STEP_WAITED()
       const float scale = gb.stage(hin, a.eps, xs, red);
       float acc[2];
       gb.dot(xs, scale, F8 ? a.sqkv + (size_t)l * qkv_rows : nullptr, n0, qkv_rows, acc);
@@ -480,11 +497,13 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
       const int grp = hb < a.heads ? hb / GRP : hb < a.heads + a.kvh ? hb - a.heads
                                                                      : hb - a.heads - a.kvh;
       signal(ctr(a, l, C_QKV + grp));
+      STEP_DONE(0, l)
       return;
     }
     r -= G.NQ;
     if (r < G.NA) {
-      att_block<GRP>(a, l, r, reinterpret_cast<float*>(xs), &flag);
+      att_block<GRP>(a, l, r, reinterpret_cast<float*>(xs), &flag, &t_w);
+      STEP_DONE(1, l)
       return;
     }
     r -= G.NA;
@@ -495,6 +514,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
       gb.load(static_cast<const uint8_t*>(a.wo) + (size_t)l * H * QD * esz, n0, H, nullptr);
       if (wid == 0) wait_for(ctr(a, l, C_ATT), 1, a.kvh, a.status, 3);
       __syncthreads();
+      STEP_WAITED()
       const float r0 = ld_wt(hin + n0), r1 = ld_wt(hin + n0 + 1);
       const float scale = gb.stage(a.att + (size_t)l * QD, a.eps, xs, red);
       float acc[2];
@@ -505,6 +525,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
         st_wt(ho + n0 + 1, r1 + acc[1]);
       }
       signal(ctr(a, l, C_O + (r & 7)));
+      STEP_DONE(2, l)
       return;
     }
     r -= G.NO;
@@ -516,6 +537,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
               a.mlp_norm + (size_t)l * H);
       if (wid == 0) wait_for(ctr(a, l, C_O), 8, G.NO, a.status, 4);
       __syncthreads();
+      STEP_WAITED()
       const float scale = gb.stage(a.ho + (size_t)l * H, a.eps, xs, red);
       float acc[2];
       gb.dot(xs, scale, F8 ? a.sgu + (size_t)l * 2 * a.F : nullptr, n0, 2 * a.F, acc);
@@ -524,6 +546,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
         st_wt(a.act + (size_t)l * a.F + (n0 >> 1), gt / (1.0f + expf(-gt)) * up);
       }
       signal(ctr(a, l, C_GU + (r & 7)));
+      STEP_DONE(3, l)
       return;
     }
     r -= G.NG;
@@ -534,12 +557,14 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
       gb.load(static_cast<const uint8_t*>(a.wd) + (size_t)l * H * a.F * esz, n0, H, nullptr);
       if (wid == 0) wait_for(ctr(a, l, C_GU), 8, G.NG, a.status, 5);
       __syncthreads();
+      STEP_WAITED()
       const float res = ld_wt(a.ho + (size_t)l * H + n0);
       const float scale = gb.stage(a.act + (size_t)l * a.F, a.eps, xs, red);
       float acc[1];
       gb.dot(xs, scale, F8 ? a.sd + (size_t)l * H : nullptr, n0, H, acc);
       if (lane == 0) st_wt(a.hd + (size_t)l * H + n0, res + acc[0]);
       signal(ctr(a, l, C_DN + (r & 7)));
+      STEP_DONE(4, l)
       return;
     }
   }
@@ -557,6 +582,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
     const uint8_t sn1 = a.seen[(size_t)slot * a.V + min(n0 + 1, a.V - 1)];
     if (wid == 0) wait_for(ctr(a, a.layers - 1, C_DN), 8, G.ND, a.status, 6);
     __syncthreads();
+    STEP_WAITED()
     const float scale = gb.stage(a.hd + (size_t)(a.layers - 1) * H, a.eps, xs, red);
     float acc[2];
     gb.dot(xs, scale, F8 ? a.slm : nullptr, n0, a.V, acc);
@@ -581,11 +607,13 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
                              __HIP_MEMORY_SCOPE_AGENT);
     }
     signal(head_c + (hb & 7) * STEP_CS);
+    STEP_DONE(5, 0)
     return;
   }
   // ---- finish (the last block): argmax over the shards, commit, reset the counters ----
   if (wid == 0) wait_for(head_c, 8, G.NH, a.status, 7);
   __syncthreads();
+  STEP_WAITED()
   __shared__ int tok_s;
   if (wid == 0) {
     unsigned long long k = __hip_atomic_load(a.best_sh + lane, __ATOMIC_RELAXED,
@@ -629,6 +657,9 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
     __hip_atomic_store(a.cnt + (size_t)i * STEP_CS, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < STEP_BEST)
     __hip_atomic_store(a.best_sh + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  STEP_DONE(6, 0)
+#undef STEP_WAITED
+#undef STEP_DONE
 }
 
 }  // namespace step
