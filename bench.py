@@ -502,7 +502,6 @@ def main():
         gemv_us[kind] = (us, nbytes)
     gu_us, gu_bytes = gemv_us["gate_up"]
     gu_gbs = gu_bytes / (gu_us * 1e-6) / 1e9
-    llm.set_option("step", 0)   # eager per-kernel profile of the per-kernel path
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(3):
         llm.decode(1, st)
@@ -513,7 +512,8 @@ def main():
     per_step_us = {k: round(1e3 * v / args.profile_steps, 2) for k, v in prof.items()}
     llm.release_row(0, st)
     st.synchronize()
-    # the same step on the per-kernel hipGraph path (A/B against the one-launch step)
+    # the same step as ONE dataflow launch (option step=1, step_kernels.hip): A/B record
+    llm.set_option("step", 1)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     llm.prefill(0, 0, prompt, 1.1, st)
     for _ in range(args.step_pos - len(prompt)):
@@ -523,11 +523,11 @@ def main():
         llm.decode(1, st)
     ev1.record(st)
     ev1.synchronize()
-    per_kernel_step_ms = ev0.elapsed_time(ev1) / 50
+    one_launch_step_ms = ev0.elapsed_time(ev1) / 50
     llm.release_row(0, st)
     st.synchronize()
-    llm.set_option("step", 1)
-    # pure decode step (one launch per token, no SNAC) against the whole-step byte roofline
+    llm.set_option("step", 0)
+    # pure decode step (graph replay, no SNAC) against the whole-step byte roofline
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n_rep = 50
     llm.prefill(0, 0, prompt, 1.1, st)
@@ -554,7 +554,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic",
             "config": {"workload": "configs[1]: Orpheus-3B bf16 single stream per GPU, "
-                                   "SNAC 24 kHz, greedy + rep-penalty 1.1, one-launch decode step",
+                                   "SNAC 24 kHz, greedy + rep-penalty 1.1, hipGraph decode step",
                        "model": "orpheus-3b (synthetic weights)", "global_batch": world,
                        "seq_len": len(prompt) + args.max_tokens, "prompt_ids": len(prompt),
                        "max_tokens": args.max_tokens, "parallelism": f"streams{world}"},
@@ -568,34 +568,20 @@ def main():
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,
             "decode_step_ms": round(step_ms, 4),
-            "decode_step_ms_per_kernel_path": round(per_kernel_step_ms, 4),
+            "decode_step_ms_one_launch_option": round(one_launch_step_ms, 4),
             "decode_tok_per_s": round(1e3 / step_ms, 1),
             "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),
                               "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4)},
-            # the dominant kernel is the one-launch B = 1 decode step itself (step_kernels.hip):
-            # one launch per token streams every weight byte + the KV cache
-            "roofline": {"kernel": "step_kernel<bf16, Orpheus-3B> (one-launch B=1 decode step: "
-                                   "28 layers + lm_head + argmax + commit)",
-                         "bound": "hbm", "achieved": round(step_bytes / step_ms / 1e6, 1),
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4),
-                         "avg_launch_us": round(step_ms * 1e3, 2), "bytes_per_launch": step_bytes,
-                         "bytes_per_launch_def": "weights 6,601,728,000 B bf16 (tied lm_head "
-                                                 "once) + KV (pos + 1) x 114,688 B, pos = "
-                                                 f"{pos} (SURVEY.md §8d)",
-                         "timing": "HIP events around 50 back-to-back launches on the engine "
-                                   "stream (bench decode_step_ms)",
-                         "traffic": pmc_traffic("step", "r03_pmc_step.json"),
-                         "traffic_source": "profiles/r03_pmc_step.json (rocprofv3 --pmc "
+            "roofline": {"kernel": "gemv1_kernel<6,2,EPI_SILU,NORM,4> (RMSNorm + gate/up + SiLU*up)",
+                         "bound": "hbm", "achieved": round(gu_gbs, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
+                         "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
+                         "traffic": pmc_traffic("gate_up"),
+                         "traffic_source": "profiles/r02_pmc_gemv.json (rocprofv3 --pmc "
                                            "FETCH_SIZE / WRITE_SIZE, separate passes)"},
-            "per_kernel_path": {
-                "note": "the per-kernel hipGraph step (option step=0; multi-row steps use it)",
-                "gate_up_gemv": {"achieved": round(gu_gbs, 1), "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
-                                 "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
-                                 "traffic": pmc_traffic("gate_up")},
-                "eager_step_us_by_kernel": per_step_us,
-                "gemv_graph_us": {k: {"us": round(v[0], 2), "GB/s": round(v[1] / v[0] / 1e3, 1)}
-                                  for k, v in gemv_us.items()}},
+            "eager_step_us_by_kernel": per_step_us,
+            "gemv_graph_us": {k: {"us": round(v[0], 2), "GB/s": round(v[1] / v[0] / 1e3, 1)}
+                              for k, v in gemv_us.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, prompt)

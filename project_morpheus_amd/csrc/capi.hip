@@ -140,7 +140,9 @@ struct mx_llm {
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
   float *attn_norm_all = nullptr, *mlp_norm_all = nullptr;
   // one-launch B = 1 step (step_kernels.hip): hand-off buffers, counters, status
-  int step = 1;                 // option: 0 = per-kernel graphs for B = 1 too (A/B)
+  int step = 0;                 // option: 1 = one-launch dataflow step for B = 1; measured
+                                // 2.57 vs 1.55 ms bf16 (profiles/r03_step_kernel_timeline_*):
+                                // the per-kernel hipGraph step stays the default
   bool step_ok = false;         // shape instantiated and buffers allocated
   int step_split_max = 0;
   float *st_hd = nullptr, *st_ho = nullptr, *st_q = nullptr, *st_kn = nullptr, *st_vn = nullptr;

@@ -114,8 +114,8 @@ def test_one_launch_step_long_context():
 
 @pytest.mark.parametrize("step", [1, 0], ids=["one_launch", "per_kernel"])
 def test_decode_parity_orpheus_width_2_layers(step):
-    """B = 1 at Orpheus widths: the one-launch dataflow step (step_kernels.hip, the default)
-    and the per-kernel hipGraph step both follow the oracle."""
+    """B = 1 at Orpheus widths: the per-kernel hipGraph step (the default) and the one-launch
+    dataflow step (step_kernels.hip, option step=1) both follow the oracle."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=0)
     prompt = [128259, 128000] + [int(x) for x in np.random.default_rng(3).integers(1000, 128000, 12)] \
