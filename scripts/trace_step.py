@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1)
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--timeline", action="store_true", help="per-stage timeline of one step")
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value")
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -33,6 +34,9 @@ def main():
                     wdtype="fp8" if args.fp8 else "bf16")
     del w
     torch.cuda.empty_cache()
+    for kv in args.opt:
+        k, v = kv.split("=")
+        llm.set_option(k, int(v))
     st = torch.cuda.Stream()
     prompt = list(range(1000, 1020))
     for r in range(R):
@@ -46,7 +50,8 @@ def main():
         llm.decode(R, st)
     e1.record(st)
     e1.synchronize()
-    print(f"rows {R} pos {args.pos}: {e0.elapsed_time(e1) / args.steps:.4f} ms/step", flush=True)
+    print(f"rows {R} pos {args.pos} {' '.join(args.opt)}: {e0.elapsed_time(e1) / args.steps:.4f} ms/step",
+          flush=True)
     if args.timeline and R == 1:
         llm.set_option("step_trace", 1)
         for _ in range(3):
