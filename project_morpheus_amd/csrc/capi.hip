@@ -92,7 +92,7 @@ struct mx_llm {
   float* rope_cos = nullptr;
   float* rope_sin = nullptr;
   int rope_rows = 0;
-  uint16_t* kcache = nullptr;  // [layers][slots+1][kvh][max_pos][128]
+  uint16_t* kcache = nullptr;  // [layers][slots+1][kvh][max_pos/32][4096] (mx_common.h kv_k_off)
   uint16_t* vcache = nullptr;
   size_t kv_layer_elems = 0;
   float *h_dec = nullptr, *h_pre = nullptr, *q = nullptr, *att = nullptr, *act = nullptr;

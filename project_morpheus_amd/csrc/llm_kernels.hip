@@ -202,16 +202,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
                 q[p + 64] = o2;
               } else {
                 uint16_t* k = a.kcache +
-                    (((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos + pos) * 128;
-                k[p] = f32_to_bf16(o1);
-                k[p + 64] = f32_to_bf16(o2);
+                    ((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos * 128;
+                k[kv_k_off(pos, p)] = f32_to_bf16(o1);
+                k[kv_k_off(pos, p + 64)] = f32_to_bf16(o2);
               }
             } else {
-              // V cache is stored transposed, [slot][kv_head][dim][pos] (see attn_kernel)
+              // fragment-major chunks (mx_common.h kv_v_off, see attn_kernel)
               uint16_t* v = a.vcache +
                   ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
-              v[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
-              v[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
+              v[kv_v_off(pos, within)] = f32_to_bf16(x1);
+              v[kv_v_off(pos, within + 1)] = f32_to_bf16(x2);
             }
           }
         }
@@ -464,15 +464,15 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
           q[p] = o1;
           q[p + 64] = o2;
         } else {
-          uint16_t* k = a.kcache + (((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos + pos) * 128;
-          k[p] = f32_to_bf16(o1);
-          k[p + 64] = f32_to_bf16(o2);
+          uint16_t* k = a.kcache + ((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos * 128;
+          k[kv_k_off(pos, p)] = f32_to_bf16(o1);
+          k[kv_k_off(pos, p + 64)] = f32_to_bf16(o2);
         }
       } else {
         uint16_t* v = a.vcache +
             ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
-        v[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
-        v[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
+        v[kv_v_off(pos, within)] = f32_to_bf16(x1);
+        v[kv_v_off(pos, within + 1)] = f32_to_bf16(x2);
       }
     }
   }
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
 //     holds position 8(r>>2) + 4T + (r&3): after the MFMA the lane (head h, group g) owns
 //     the scores of positions 8g .. 8g+7, which is exactly its A fragment for P.V.
 //   * O^T += P V with the same instruction: A = P (three bf16 parts, lane-local, no data
-//     movement), B = V^T fragments.  The V cache is kept TRANSPOSED ([slot][kvh][dim][pos])
+//     movement), B = V^T fragments.  The V cache chunks are stored in that fragment order (kv_v_off)
 //     so a lane's B fragment (8 consecutive positions of one dim) is one 16-byte load.
 //   Waves merge in LDS; with several splits the block publishes (m, l, acc) with
 //   write-through (sc1) stores, takes a ticket on a per-(row, kv-head) counter and the last
@@ -538,23 +538,25 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
   const int c = lane & 15, g = lane >> 4;
   const int slot = a.row_slot[r];
   const size_t head = (size_t)slot * a.kv_heads + kvh;
-  const uint4* K = reinterpret_cast<const uint4*>(a.kcache) + head * a.max_pos * 16;
-  const uint16_t* VT = a.vcache + head * 128 * a.max_pos;
-  const int rr = lane & 15;
+  // K and V in fragment-major 32-position chunks (mx_common.h kv_k_off / kv_v_off): every
+  // fragment load below is one lane-linear 1 KB run
+  const uint4* Kf = reinterpret_cast<const uint4*>(a.kcache) + head * a.max_pos * 16;
+  const uint4* Vf = reinterpret_cast<const uint4*>(a.vcache) + head * a.max_pos * 16;
 
   // K fragments (A operand): tile T, MFMA row rr -> position 8(rr>>2) + 4T + (rr&3);
-  // V^T fragments (B operand): lane (dim 16 t + c, group g) <- positions base + 8g .. +8
+  // V fragments (B operand): lane (dim 16 t + c, group g) <- positions base + 8g .. +8.
+  // Positions of the last chunk at or past L hold stale (finite) cache data: their scores are
+  // masked to -inf below, so their P is exactly 0.
   uint4 kf[2][2][4], vf[2][8];
   auto load_kv = [&](int base, int b) {
+    const uint4* kc = Kf + (size_t)(base >> 5) * 512 + lane;
+    const uint4* vc = Vf + (size_t)(base >> 5) * 512 + lane;
 #pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      const int p = min(base + 8 * (rr >> 2) + 4 * T + (rr & 3), L - 1);
+    for (int T = 0; T < 2; ++T)
 #pragma unroll
-      for (int st = 0; st < 4; ++st) kf[b][T][st] = K[(size_t)p * 16 + 4 * st + g];
-    }
+      for (int st = 0; st < 4; ++st) kf[b][T][st] = kc[(T * 4 + st) * 64];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-      vf[b][t] = *reinterpret_cast<const uint4*>(VT + (size_t)(16 * t + c) * a.max_pos + base + 8 * g);
+    for (int t = 0; t < 8; ++t) vf[b][t] = vc[t * 64];
   };
   // chunks are dealt round-robin over the waves (wave w: chunks w, w + NW, ...), so a split
   // longer than the context still keeps every wave busy with ~equal work

@@ -75,4 +75,21 @@ __device__ __forceinline__ uint4 load_nt(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// KV cache layout.  One (slot, kv head) holds max_pos x 128 bf16 of K and the
+// same of V, stored in chunks of 32 positions (4,096 elements), each chunk in the order the
+// attention MFMAs consume it, so that every wave load instruction reads 1 KB contiguous
+// (lane-linear 16-byte pieces) instead of 16 rows x 64 B:
+//   K chunk [T 2][st 4][g 4][rr 16][8 dims]: MFMA row rr of tile T is position
+//     8 (rr >> 2) + 4 T + (rr & 3) of the chunk, k-step st / group g hold dims 32 st + 8 g + j;
+//   V chunk [t 8][g 4][c 16][8 positions]: dim 16 t + c, positions 8 g .. 8 g + 7.
+__device__ __forceinline__ size_t kv_k_off(int p, int d) {
+  const int q = p & 31;
+  const int rr = 4 * (q >> 3) + (q & 3), T = (q >> 2) & 1;
+  return (size_t)(p >> 5) * 4096 + (size_t)((((T * 4 + (d >> 5)) * 64 + ((d >> 3) & 3) * 16 + rr) << 3) + (d & 7));
+}
+__device__ __forceinline__ size_t kv_v_off(int p, int d) {
+  const int q = p & 31;
+  return (size_t)(p >> 5) * 4096 + (size_t)(((((d >> 4) * 4 + (q >> 3)) * 16 + (d & 15)) << 3) + (q & 7));
+}
+
 }  // namespace mx

@@ -44,7 +44,7 @@ struct GemvArgs {
   const float* rope_sin;
   const int32_t* row_slot;
   const int32_t* row_pos;
-  uint16_t* kcache;        // this layer: [slots][kv_heads][max_pos][128]
+  uint16_t* kcache;        // this layer: [slots][kv_heads][max_pos * 128], 32-position chunks (kv_k_off)
   uint16_t* vcache;
   int heads, kv_heads, max_pos;
   float* Q;                // [R][heads][128]
@@ -65,7 +65,7 @@ struct GemvArgs {
 struct AttnArgs {
   const float* Q;          // [R][heads][128]
   const uint16_t* kcache;  // this layer
-  const uint16_t* vcache;  // TRANSPOSED: [slot][kv_head][128][max_pos]
+  const uint16_t* vcache;  // the same, V chunks in P.V fragment order (kv_v_off)
   const int32_t* row_slot;
   const int32_t* row_pos;
   int heads, kv_heads, max_pos;

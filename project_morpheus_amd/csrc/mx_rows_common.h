@@ -83,15 +83,15 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
               q[p + 64] = o2;
             } else {
               uint16_t* kc = a.kcache +
-                  (((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos + pos) * 128;
-              kc[p] = f32_to_bf16(o1);
-              kc[p + 64] = f32_to_bf16(o2);
+                  ((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos * 128;
+              kc[kv_k_off(pos, p)] = f32_to_bf16(o1);
+              kc[kv_k_off(pos, p + 64)] = f32_to_bf16(o2);
             }
           } else {
             uint16_t* vc = a.vcache +
                 ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
-            vc[(size_t)within * a.max_pos + pos] = f32_to_bf16(x1);
-            vc[(size_t)(within + 1) * a.max_pos + pos] = f32_to_bf16(x2);
+            vc[kv_v_off(pos, within)] = f32_to_bf16(x1);
+            vc[kv_v_off(pos, within + 1)] = f32_to_bf16(x2);
           }
         }
       } else if (EPI == EPI_ARGMAX) {

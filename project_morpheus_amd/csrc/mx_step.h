@@ -19,7 +19,7 @@ struct StepArgs {
   const float *attn_norm, *mlp_norm, *norm;  // [L][H], [L][H], [H]
   const uint16_t* embed;                     // bf16 [V][H] (next-token gather)
   const float *rope_cos, *rope_sin;          // [max_pos][64]
-  uint16_t *kcache, *vcache;                 // [L][slots][kvh][max_pos][128], V transposed
+  uint16_t *kcache, *vcache;                 // [L][slots][kvh][max_pos * 128], fragment-major chunks
   size_t kv_layer_elems;
   // row / slot state (row 0)
   int32_t *row_slot, *row_pos, *row_token;

@@ -242,22 +242,28 @@ __device__ void att_block(const StepArgs& a, int l, int idx, float* lds, int* fl
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int pos = a.row_pos[0], slot = a.row_slot[0];
   const size_t head = (size_t)slot * a.kvh + g;
-  const uint16_t* K = a.kcache + a.kv_layer_elems * l + head * a.max_pos * 128;
-  const uint16_t* VT = a.vcache + a.kv_layer_elems * l + head * 128 * a.max_pos;
+  // fragment-major 32-position chunks (mx_common.h kv_k_off / kv_v_off), in 16-byte units
+  const uint4* Kf = reinterpret_cast<const uint4*>(a.kcache + a.kv_layer_elems * l) + head * a.max_pos * 16;
+  const uint4* Vf = reinterpret_cast<const uint4*>(a.vcache + a.kv_layer_elems * l) + head * a.max_pos * 16;
   const int p0 = s * STEP_SPLIT + wid * 16;
   const int pp = lane >> 2, dq = (lane & 3) * 32;
   const int p = p0 + pp;
   const bool valid = p < pos;
   uint4 kr[4], vr[2][2];
   {
-    const uint4* kp = reinterpret_cast<const uint4*>(K + (size_t)max(min(p, pos - 1), 0) * 128 + dq);
+    // lane: position p, dims dq .. dq + 31 = k-step dq / 32, groups i = 0..3
+    const int pk = max(min(p, pos - 1), 0), q = pk & 31;
+    const uint4* kp = Kf + (size_t)(pk >> 5) * 512 + (((q >> 2) & 1) * 4 + (dq >> 5)) * 64 +
+                      4 * (q >> 3) + (q & 3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) kr[i] = kp[i];
+    for (int i = 0; i < 4; ++i) kr[i] = kp[16 * i];
+    // lane: dims 2 lane + j, positions p0 .. p0 + 15 (two groups of 8; p0 is a multiple of 16)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const uint4* vp = reinterpret_cast<const uint4*>(VT + (size_t)(2 * lane + j) * a.max_pos + p0);
+      const int d = 2 * lane + j;
+      const uint4* vp = Vf + (size_t)(p0 >> 5) * 512 + ((d >> 4) * 4 + ((p0 & 31) >> 3)) * 16 + (d & 15);
       vr[j][0] = vp[0];
-      vr[j][1] = vp[1];
+      vr[j][1] = vp[16];
     }
   }
   float* qs = lds;                   // [GRP][128]
@@ -474,10 +480,10 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
           } else {
             const int kv = hh - a.heads;
             uint16_t* k = a.kcache + a.kv_layer_elems * l +
-                          (((size_t)slot * a.kvh + kv) * a.max_pos + pos) * 128;
+                          ((size_t)slot * a.kvh + kv) * a.max_pos * 128;
             const uint16_t b1 = f32_to_bf16(o1), b2 = f32_to_bf16(o2);
-            k[pr] = b1;
-            k[pr + 64] = b2;
+            k[kv_k_off(pos, pr)] = b1;
+            k[kv_k_off(pos, pr + 64)] = b2;
             float* kn = a.knew + ((size_t)l * a.kvh + kv) * 128;
             st_wt(kn + pr, bf16_to_f32(b1));
             st_wt(kn + pr + 64, bf16_to_f32(b2));
@@ -486,8 +492,8 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
           const int kv = hh - a.heads - a.kvh;
           uint16_t* v = a.vcache + a.kv_layer_elems * l + ((size_t)slot * a.kvh + kv) * 128 * a.max_pos;
           const uint16_t b1 = f32_to_bf16(x1), b2 = f32_to_bf16(x2);
-          v[(size_t)within * a.max_pos + pos] = b1;
-          v[(size_t)(within + 1) * a.max_pos + pos] = b2;
+          v[kv_v_off(pos, within)] = b1;
+          v[kv_v_off(pos, within + 1)] = b2;
           float* vn = a.vnew + ((size_t)l * a.kvh + kv) * 128;
           st_wt(vn + within, bf16_to_f32(b1));
           st_wt(vn + within + 1, bf16_to_f32(b2));

@@ -16,7 +16,12 @@ step() {
   if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
   return 0
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step tests 600 python -u -m pytest tests/test_gpu_llm.py tests/test_gpu_fp8.py tests/test_gpu_batching.py -m gpu -k "batched or rows or fp8 or batch" -v -p no:cacheprovider --timeout 170 --timeout-method thread
+if [ "${ALL_TESTS:-0}" = 1 ]; then
+  step tests 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 170 --timeout-method thread
+elif [ "${SKIP_TESTS:-0}" != 1 ]; then
+  step tests 600 python -u -m pytest tests/test_gpu_llm.py tests/test_gpu_fp8.py tests/test_gpu_batching.py -m gpu -k "batched or rows or fp8 or batch" -v -p no:cacheprovider --timeout 170 --timeout-method thread
+fi
+step r1 200 python scripts/trace_step.py --rows 1 --steps 50
 step r32 200 python scripts/trace_step.py --rows 32 --steps 20
 step r64 200 python scripts/trace_step.py --rows 64 --steps 20
 step r8f8 200 python scripts/trace_step.py --rows 8 --fp8 --steps 20
