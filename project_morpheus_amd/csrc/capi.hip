@@ -140,9 +140,10 @@ struct mx_llm {
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
   float *attn_norm_all = nullptr, *mlp_norm_all = nullptr;
   // one-launch B = 1 step (step_kernels.hip): hand-off buffers, counters, status
-  int step = 0;                 // option: 1 = one-launch dataflow step for B = 1; measured
-                                // 2.57 vs 1.55 ms bf16 (profiles/r03_step_kernel_timeline_*):
-                                // the per-kernel hipGraph step stays the default
+  int step = 0;                 // option: 1 = one-launch dataflow step for B = 1 (measured
+                                // 2.57 vs 1.55 ms bf16, profiles/r03_step_kernel_timeline_*),
+                                // 2 = the same roles cut into per-layer launches (step_cuts)
+  int step_cuts = 9;            // option (step = 2): launches start at qkv and gate/up
   bool step_ok = false;         // shape instantiated and buffers allocated
   int step_split_max = 0;
   float *st_hd = nullptr, *st_ho = nullptr, *st_q = nullptr, *st_kn = nullptr, *st_vn = nullptr;
@@ -856,7 +857,8 @@ static hipError_t enqueue_step(mx_llm* x, hipStream_t st) {
   a.commit = sample ? 0 : 1;
   a.trace = x->st_trace;
   x->st_last_blocks = step_blocks(a);
-  hipError_t e = launch_step(a, c.wdtype == WT_FP8, st);
+  hipError_t e = x->step == 2 ? launch_step_cut(a, c.wdtype == WT_FP8, x->step_cuts, st)
+                              : launch_step(a, c.wdtype == WT_FP8, st);
   if (e != hipSuccess || !sample) return e;
   SampleArgs sa{};
   sa.logits = x->logits; sa.row_slot = x->row_slot; sa.row_pos = x->row_pos;
@@ -1081,8 +1083,11 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
   } else if (k == "step") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "step must be 0 or 1");
+    if (value < 0 || value > 2) MX_FAIL(x, MX_ERR_ARG, "step must be 0, 1 or 2");
     x->step = value;
+  } else if (k == "step_cuts") {  // step = 2: stage starts that begin a launch (mx_step.h)
+    if (value < 1 || value > 31 || !(value & 1)) MX_FAIL(x, MX_ERR_ARG, "step_cuts: 5-bit mask with bit 0 set");
+    x->step_cuts = value;
   } else if (k == "step_trace") {  // diagnostic: per-block timeline of one-launch steps
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "step_trace must be 0 or 1");
     if (value && !x->st_trace && x->step_ok) {

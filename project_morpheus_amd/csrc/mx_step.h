@@ -44,6 +44,7 @@ struct StepArgs {
   float eps, att_scale;
   int commit;                                // 1: finish commits the argmax (greedy row)
   unsigned long long* trace;                 // diagnostic: [blocks][4] timestamps (null: off)
+  int64_t block0;                            // global role index of this launch's block 0
 };
 
 // Blocks of the launch: layers * (qkv + attention + o + gate/up + down) + lm_head + 1.
@@ -52,6 +53,11 @@ size_t step_counter_ints(int layers);
 // hipErrorNotSupported when the shape has no instantiation (the caller keeps the per-kernel
 // step); the launch itself is asynchronous on `st`.
 hipError_t launch_step(const StepArgs& a, bool f8, hipStream_t st);
+// The same step cut into several launches (stream-ordered, same roles and counters): a layer's
+// stages are qkv 0, attention 1, o-proj 2, gate/up 3, down 4; bit s of `cuts` starts a new
+// launch at stage s of every layer (bit 0 is implied), and the lm_head + finish blocks are one
+// more launch.  Blocks still wait only on lower role indices, now possibly in an earlier launch.
+hipError_t launch_step_cut(const StepArgs& a, bool f8, int cuts, hipStream_t st);
 bool step_supported(int H, int F, int heads, int kvh, bool f8);
 
 }  // namespace mx

@@ -445,7 +445,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs a) {
     tr_[3] = ((unsigned long long)(role_) << 32) | (unsigned)(layer_);              \
   }
   const Geo G(a);
-  const int64_t b = blockIdx.x;
+  const int64_t b = blockIdx.x + a.block0;
   const int H = a.H, QD = a.heads * 128;
   const int esz = F8 ? 1 : 2;
   const int qkv_rows = QD + 2 * a.kvh * 128;
@@ -696,13 +696,15 @@ bool step_supported(int H, int F, int heads, int kvh, bool f8) {
   return false;
 }
 
-hipError_t launch_step(const StepArgs& a, bool f8, hipStream_t st) {
+// blocks [b0, b0 + nb) of the step's role list as one launch
+static hipError_t launch_step_range(StepArgs a, bool f8, int64_t b0, int64_t nb, hipStream_t st) {
   if (a.heads * 128 != a.H || a.kvh > 8 || a.heads % a.kvh || a.nsplit < 1 ||
       a.nsplit > a.split_max || a.split_max > step::STEP_MAX_SPLITS)
     return hipErrorInvalidValue;
   const int grp = a.heads / a.kvh;
-  const int64_t nb = step_blocks(a);
-  if (nb >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  if (nb < 1 || b0 < 0 || b0 + nb > step_blocks(a) || nb >= (int64_t)1 << 31)
+    return hipErrorInvalidValue;
+  a.block0 = b0;
 #define MX_S(F8_, H_, F_, G_)                                                               \
   if (f8 == F8_ && a.H == H_ && a.F == F_ && grp == G_) {                                   \
     constexpr int E_ = F8_ ? 1024 : 512;                                                    \
@@ -713,6 +715,27 @@ hipError_t launch_step(const StepArgs& a, bool f8, hipStream_t st) {
   MX_STEP_SHAPES(MX_S)
 #undef MX_S
   return hipErrorNotSupported;
+}
+
+hipError_t launch_step(const StepArgs& a, bool f8, hipStream_t st) {
+  return launch_step_range(a, f8, 0, step_blocks(a), st);
+}
+
+hipError_t launch_step_cut(const StepArgs& a, bool f8, int cuts, hipStream_t st) {
+  const step::Geo G(a);
+  const int64_t s0[6] = {0, G.NQ, G.NQ + G.NA, G.NQ + G.NA + G.NO, G.NQ + G.NA + G.NO + G.NG, G.P};
+  cuts |= 1;
+  for (int l = 0; l < a.layers; ++l) {
+    int s = 0;
+    while (s < 5) {
+      int e = s + 1;
+      while (e < 5 && !((cuts >> e) & 1)) ++e;
+      const hipError_t r = launch_step_range(a, f8, (int64_t)l * G.P + s0[s], s0[e] - s0[s], st);
+      if (r != hipSuccess) return r;
+      s = e;
+    }
+  }
+  return launch_step_range(a, f8, (int64_t)a.layers * G.P, G.NH + 1, st);
 }
 
 }  // namespace mx

@@ -93,14 +93,18 @@ def test_long_prefill_multi_split_small():
     assert _compare(cfg, w, prompt, 90) >= 60
 
 
-@pytest.mark.parametrize("step", [1, 0], ids=["one_launch", "per_kernel"])
+STEP_MODES = [{"step": 1}, {"step": 0}, {"step": 2, "step_cuts": 9}, {"step": 2, "step_cuts": 31}]
+STEP_IDS = ["one_launch", "per_kernel", "cut_qkv_gu", "cut_every_stage"]
+
+
+@pytest.mark.parametrize("step", STEP_MODES, ids=STEP_IDS)
 def test_long_context_many_splits_small(step):
     """250-token prompt (2 prefill splits of 128) then 150 steps: L reaches 400 -> 4 splits of
     the per-kernel path's ticket merge, 4-7 64-position splits of the one-launch step's merge."""
     cfg = _cfgs("small")
     w = synthetic_llm_weights(cfg, seed=13, std=0.05, norm_jitter=0.5)
     prompt = [int(x) for x in np.random.default_rng(4).integers(0, cfg.vocab, 250)]
-    assert _compare(cfg, w, prompt, 150, options={"step": step}) >= 100
+    assert _compare(cfg, w, prompt, 150, options=step) >= 100
 
 
 def test_one_launch_step_long_context():
@@ -112,15 +116,16 @@ def test_one_launch_step_long_context():
     assert _compare(cfg, w, prompt, 1010, options={"step": 1}, max_pos=1280) >= 600
 
 
-@pytest.mark.parametrize("step", [1, 0], ids=["one_launch", "per_kernel"])
+@pytest.mark.parametrize("step", STEP_MODES, ids=STEP_IDS)
 def test_decode_parity_orpheus_width_2_layers(step):
-    """B = 1 at Orpheus widths: the per-kernel hipGraph step (the default) and the one-launch
-    dataflow step (step_kernels.hip, option step=1) both follow the oracle."""
+    """B = 1 at Orpheus widths: the per-kernel hipGraph step (the default), the one-launch
+    dataflow step (step_kernels.hip, option step=1) and its roles cut into per-layer launches
+    (step=2) all follow the oracle."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=0)
     prompt = [128259, 128000] + [int(x) for x in np.random.default_rng(3).integers(1000, 128000, 12)] \
         + [128009, 128260, 128261, 128257]
-    assert _compare(cfg, w, prompt, 24, options={"step": step}) >= 20
+    assert _compare(cfg, w, prompt, 24, options=step) >= 20
 
 
 def _orpheus_prompt(n_text, seed):
