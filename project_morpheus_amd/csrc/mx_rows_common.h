@@ -29,12 +29,67 @@ __device__ __forceinline__ void split_parts(float* x, bf16x8* f) {
   }
 }
 
+// Operands of the epilogue that do not depend on the GEMM result, loaded BEFORE the split-K
+// hand-off (drain, ticket, merge loads) so that their round trips -- two dependent ones for
+// RoPE (row position, then the table) -- overlap it instead of following it.
+template <int MT, int NT, int EPI>
+struct EpiPre {
+  float y[EPI == EPI_RESID ? MT : 1][EPI == EPI_RESID ? NT : 1][4];    // RESID: Y before the add
+  float cs[EPI == EPI_QKV ? MT : 1][EPI == EPI_QKV ? NT : 1][2];       // QKV: RoPE per pair
+  float sn[EPI == EPI_QKV ? MT : 1][EPI == EPI_QKV ? NT : 1][2];
+  int slot[EPI == EPI_QKV ? NT : 1], pos[EPI == EPI_QKV ? NT : 1];
+  float ws[MT][4];                                                      // fp8 row scales
+};
+
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void rows_epilogue_pre(const GemvArgs& a, EpiPre<MT, NT, EPI>& P,
+                                                  int n0, int r0, int c, int g) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int nb = n0 + 16 * mt + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P.ws[mt][i] = a.wdtype == WT_FP8 ? a.wscale[min(nb + i, a.N - 1)] : 1.f;
+  }
+  if (EPI == EPI_RESID) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int b = min(r0 + 16 * nt + c, a.R - 1);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int nb = min(n0 + 16 * mt + 4 * g, a.N - 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) P.y[mt % (EPI == EPI_RESID ? MT : 1)][nt % (EPI == EPI_RESID ? NT : 1)][i] =
+            a.Y[(size_t)b * a.ystride + nb + i];
+      }
+    }
+  } else if (EPI == EPI_QKV) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int b = min(r0 + 16 * nt + c, a.R - 1);
+      P.slot[nt % (EPI == EPI_QKV ? NT : 1)] = a.row_slot[b];
+      P.pos[nt % (EPI == EPI_QKV ? NT : 1)] = a.row_pos[b];
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int n = n0 + 16 * mt + 4 * g + i;
+          const int p = (n & 127) >> 1;
+          const size_t ix = (size_t)P.pos[nt % (EPI == EPI_QKV ? NT : 1)] * 64 + p;
+          P.cs[mt % (EPI == EPI_QKV ? MT : 1)][nt % (EPI == EPI_QKV ? NT : 1)][i >> 1] = a.rope_cos[ix];
+          P.sn[mt % (EPI == EPI_QKV ? MT : 1)][nt % (EPI == EPI_QKV ? NT : 1)][i >> 1] = a.rope_sin[ix];
+        }
+  }
+}
+
 // Epilogue of one wave's tile: lane (batch col c, group g) holds weight rows
 // n0 + 16 mt + 4 g + i for batch rows r0 + 16 nt + c (MFMA C/D layout).
 template <int MT, int NT, int EPI>
 __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT][NT],
                                               const float (&scale)[NT], int n0, int r0, int c,
-                                              int g) {
+                                              int g, const EpiPre<MT, NT, EPI>& P) {
   unsigned long long best[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) best[nt] = 0ull;
@@ -50,7 +105,7 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
       for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] * scale[nt];
       if (a.wdtype == WT_FP8) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] *= a.wscale[min(nb + i, a.N - 1)];
+        for (int i = 0; i < 4; ++i) v[i] *= P.ws[mt][i];
       }
       if (!bok || nb >= a.N) continue;
       if (EPI == EPI_STORE) {
@@ -58,7 +113,9 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
         for (int i = 0; i < 4; ++i) a.Y[(size_t)b * a.ystride + nb + i] = v[i];
       } else if (EPI == EPI_RESID) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a.Y[(size_t)b * a.ystride + nb + i] += v[i];
+        for (int i = 0; i < 4; ++i)
+          a.Y[(size_t)b * a.ystride + nb + i] =
+              P.y[mt % (EPI == EPI_RESID ? MT : 1)][nt % (EPI == EPI_RESID ? NT : 1)][i] + v[i];
       } else if (EPI == EPI_SILU) {
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
@@ -66,15 +123,16 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
           a.Y[(size_t)b * (a.N >> 1) + ((nb + i) >> 1)] = gt / (1.0f + expf(-gt)) * up;
         }
       } else if (EPI == EPI_QKV) {
-        const int slot = a.row_slot[b], pos = a.row_pos[b];
+        const int slot = P.slot[nt % (EPI == EPI_QKV ? NT : 1)];
+        const int pos = P.pos[nt % (EPI == EPI_QKV ? NT : 1)];
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
           const int n = nb + i;
           const int hh = n >> 7, within = n & 127, p = within >> 1;
           const float x1 = v[i], x2 = v[i + 1];
           if (hh < a.heads + a.kv_heads) {
-            const float cs = a.rope_cos[(size_t)pos * 64 + p];
-            const float sn = a.rope_sin[(size_t)pos * 64 + p];
+            const float cs = P.cs[mt % (EPI == EPI_QKV ? MT : 1)][nt % (EPI == EPI_QKV ? NT : 1)][i >> 1];
+            const float sn = P.sn[mt % (EPI == EPI_QKV ? MT : 1)][nt % (EPI == EPI_QKV ? NT : 1)][i >> 1];
             const float o1 = x1 * cs - x2 * sn;
             const float o2 = x2 * cs + x1 * sn;
             if (hh < a.heads) {
