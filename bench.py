@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--fp8-batch", type=int, default=8,
                    help="configs[4]: fp8 streams per GPU (0 skips the fp8 section)")
     p.add_argument("--no-http", action="store_true", help="skip the HTTP-level line")
+    p.add_argument("--compaction-ab", action="store_true",
+                   help="also run configs[2] without decode-row compaction (A/B record)")
     p.add_argument("--long-read-docs", type=int, default=16,
                    help="configs[3]: long_read documents (0 skips it)")
     p.add_argument("--step-pos", type=int, default=600,
@@ -117,7 +119,8 @@ def cpu_baseline(cfg, prompt, n_decode=6, mid_pos=610):
             "tok_per_s": round(1.0 / t_tok, 3)}
 
 
-def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, label=None):
+def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, label=None,
+                compact=True):
     """configs[2]: ``n_streams`` (default ``args.batch``) utterances per GPU arriving with
     exponential gaps (mean 10 ms, seed 4), synthetic prompts of 16-64 ids, ``max_tokens``
     each, served by the continuous-batching loop; aggregate RTF = all audio / wall time
@@ -128,7 +131,7 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
 
     from project_morpheus_amd import inference as I
     from project_morpheus_amd.batching import BatchSynthesizer, StreamRequest
-    syn = BatchSynthesizer(llm, snac, seed=rank)
+    syn = BatchSynthesizer(llm, snac, seed=rank, compact=compact)
     rng = np.random.default_rng(4 + 1000 * rank)
 
     def requests():
@@ -148,7 +151,10 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
         dist.barrier()
     torch.cuda.synchronize()
     reqs = requests()
+    syn.row_steps.clear()
     wall = syn.run(reqs)
+    steps = sum(syn.row_steps.values())
+    row_steps = sum(k * v for k, v in syn.row_steps.items())
     torch.cuda.synchronize()
     audio = sum(r.audio_seconds for r in reqs)
     firsts = [r.first_audio_ms for r in reqs]
@@ -168,7 +174,8 @@ def run_batched(args, llm, snac, prompt, rank, world, dist, n_streams=None, labe
             "unit": "audio-sec/wall-sec", "wall_s": round(wall, 3),
             "audio_seconds": round(audio, 2),
             "p50_first_audio_ms": round(statistics.median(firsts), 2),
-            "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1)}
+            "tok_per_s": round(n_streams * world * args.max_tokens / wall, 1),
+            "decode_steps": steps, "mean_rows_per_step": round(row_steps / max(1, steps), 2)}
 
 
 async def _asgi_speech(app, text: str):
@@ -477,9 +484,13 @@ def main():
         ceiling = {u: run_orchestrator_ceiling(utt_s, u) for u in ("bytes", "ms")}
 
     # ---- configs[2]: B concurrent streams per GPU, continuous batching + batched SNAC ----
-    batched = None
+    batched = batched_nc = None
     if B3 > 0:
         batched = run_batched(args, llm, snac, prompt, rank, world, dist)
+        if args.compaction_ab:
+            batched_nc = run_batched(args, llm, snac, prompt, rank, world, dist,
+                                     label="configs[2] without decode-row compaction",
+                                     compact=False)
 
     # ---- configs[3]: long_read documents sharded over the ranks, gathered + stitched ----
     long_read = None
@@ -565,6 +576,7 @@ def main():
             "http_level_service": http_service,
             "orchestrator_ceiling": ceiling,
             "configs_2_batched": batched,
+            **({"configs_2_no_compaction": batched_nc} if batched_nc else {}),
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,
             "decode_step_ms": round(step_ms, 4),

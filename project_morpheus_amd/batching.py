@@ -32,6 +32,8 @@ adapters use; a background thread owns the GPU).
 """
 from __future__ import annotations
 
+import collections
+
 import queue
 import threading
 import time
@@ -204,6 +206,7 @@ class BatchSynthesizer:
             raise ValueError("BatchSynthesizer needs one KV slot per decode row")
         self.llm, self.snac, self.seed = llm, snac, seed
         self.compact = compact  # row compaction (mx_llm_move_row) when streams end
+        self.row_steps = collections.Counter()  # decode steps issued per row count (stats)
         self.depth = max(1, BATCH_DEPTH if depth is None else depth)
         # SNAC window coalescing: due windows are held until `snac_min_batch` of them are
         # ready or the oldest has waited `snac_max_hold` decode steps (a stream's first window
@@ -488,6 +491,7 @@ class BatchSynthesizer:
             while act and len(inflight) < self.depth:
                 n_rows = max(r.idx for r in act) + 1
                 llm.decode(n_rows, self.stream)
+                self.row_steps[n_rows] += 1
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 entries = []
