@@ -78,50 +78,71 @@ __global__ __launch_bounds__(256) void snac_embed_kernel(const int32_t* frames, 
 // Depthwise k7 dilated conv, "same" padding 3*dil, optional Snake on input and output, on
 // channels-last activations [B][T][C] (every SNAC activation is channels-last, so a conv-GEMM
 // B fragment -- 8 consecutive channels at one time step -- is two 16-byte loads).
-// Block = 64 channels x 4 time rows; the TT-step output tile reads a haloed Snake(x) tile
-// staged once in LDS (Snake evaluated once per input).  Grid (ceil(T/TT), C/64, B): TT = 64
-// for the batched shapes, 16 for single windows (4x the blocks; the halo costs more there).
+// Block = 64 channels x 16 time rows, 4 channels (one 16-byte piece) per lane, so a wave's
+// load or store instruction moves 4 rows x 256 B = 1 KB (with one channel per lane it moved
+// 256 B: dwconv_kernel<64> ran at 4.1 TB/s on the 32-window shapes).  The TT-step output tile
+// reads a haloed Snake(x) tile staged once in LDS (Snake evaluated once per input).  Grid
+// (ceil(T/TT), C/64, B): TT = 64 for the batched shapes, 16 for single windows.
 // ---------------------------------------------------------------------------------
 template <int TT>
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* x, float* y, const float* w,
                                                      const float* b, const float* ain,
                                                      const float* aout, int C, int T, int dil) {
-  const int cl = threadIdx.x & 63, tr = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + cl, t0 = blockIdx.x * TT, bt = blockIdx.z;
+  const int cq = threadIdx.x & 15, tr = threadIdx.x >> 4;  // channel quad, row group (16)
+  const int c = blockIdx.y * 64 + 4 * cq, t0 = blockIdx.x * TT, bt = blockIdx.z;
   const int halo = 3 * dil;
-  __shared__ float tile[TT + 54][64];
+  __shared__ float4 tile[TT + 54][16];
   const float* xb = x + (size_t)bt * T * C + c;
-  const float a_in = ain ? ain[c] : 0.f;
+  const float4 a_in = ain ? *reinterpret_cast<const float4*>(ain + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   // every global load of the haloed tile is issued before any is consumed (a runtime-count
-  // loop of load -> Snake -> LDS store paid one memory latency per row: ~11-15 us per launch
-  // for a single window regardless of its size)
-  constexpr int NI = (TT + 54 + 3) / 4;
+  // loop of load -> Snake -> LDS store paid one memory latency per row)
+  constexpr int NI = (TT + 54 + 15) / 16;
   const int rows = TT + 2 * halo;
-  float v[NI];
+  float4 v[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int i = tr + 4 * j, t = t0 - halo + i;
-    v[j] = (i < rows && t >= 0 && t < T) ? xb[(size_t)t * C] : 0.f;
+    const int i = tr + 16 * j, t = t0 - halo + i;
+    v[j] = (i < rows && t >= 0 && t < T) ? *reinterpret_cast<const float4*>(xb + (size_t)t * C)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int i = tr + 4 * j;
-    if (i < rows) tile[i][cl] = ain ? snake(v[j], a_in) : v[j];
+    const int i = tr + 16 * j;
+    if (i < rows) {
+      float4 u = v[j];
+      if (ain) {
+        u.x = snake(u.x, a_in.x); u.y = snake(u.y, a_in.y);
+        u.z = snake(u.z, a_in.z); u.w = snake(u.w, a_in.w);
+      }
+      tile[i][cq] = u;
+    }
   }
   __syncthreads();
-  float wk[7];
+  float wk[7][4];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) wk[k] = w[c * 7 + k];
-  const float bias = b[c], a_out = aout ? aout[c] : 0.f;
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wk[k][e] = w[(c + e) * 7 + k];
+  const float4 bias = *reinterpret_cast<const float4*>(b + c);
+  const float4 a_out = aout ? *reinterpret_cast<const float4*>(aout + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   float* yb = y + (size_t)bt * T * C + c;
-  for (int i = tr; i < TT; i += 4) {
+  for (int i = tr; i < TT; i += 16) {
     const int t = t0 + i;
     if (t >= T) break;
-    float acc = bias;
+    float4 acc = bias;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) acc = fmaf(wk[k], tile[i + k * dil][cl], acc);
-    if (aout) acc = snake(acc, a_out);
-    yb[(size_t)t * C] = acc;
+    for (int k = 0; k < 7; ++k) {
+      const float4 u = tile[i + k * dil][cq];
+      acc.x = fmaf(wk[k][0], u.x, acc.x);
+      acc.y = fmaf(wk[k][1], u.y, acc.y);
+      acc.z = fmaf(wk[k][2], u.z, acc.z);
+      acc.w = fmaf(wk[k][3], u.w, acc.w);
+    }
+    if (aout) {
+      acc.x = snake(acc.x, a_out.x); acc.y = snake(acc.y, a_out.y);
+      acc.z = snake(acc.z, a_out.z); acc.w = snake(acc.w, a_out.w);
+    }
+    *reinterpret_cast<float4*>(yb + (size_t)t * C) = acc;
   }
 }
 
@@ -448,8 +469,14 @@ hipError_t launch_split_planes(const float* src, uint16_t* dst, int64_t n, hipSt
 // Output stage: conv 64->1 k7 pad 3 (+bias) -> tanh on the Snake-activated input (the
 // last ResidualUnit's epilogue wrote Snake(x, out.alpha)), then the PCM16 epilogue on the
 // [lo, hi) slice: (x * 32767) truncated toward zero, as (audio_slice*32767).to(int16).
-// Grid (ceil(T/64), B), block 256: 4 lanes per output sample split the 64 channels.
+// Grid (ceil(T / OUT_T), B), block 256.  The block stages its input rows [t0 - 3, t0 + OUT_T
+// + 3) (channels-last, 256 B per row) in LDS with coalesced 16-byte loads, then 16 lanes share
+// one output sample: lane j holds channels 4j .. 4j+3 of the 7 taps' weights in registers, reads
+// one 16-byte piece per tap (a row is 256 contiguous bytes: conflict-free), and the 16 partial
+// sums meet by butterfly.  (One thread per sample straight from global memory touched 16-64
+// cache lines per load instruction: 139 us for 32 windows, against ~20 us of HBM bytes.)
 // ---------------------------------------------------------------------------------
+constexpr int OUT_T = 256;
 __global__ __launch_bounds__(256) void snac_out_kernel(const float* xs, const float* w,
                                                        const float* b, int T, int lo, int hi,
                                                        float* audio, int16_t* pcm,
@@ -458,36 +485,57 @@ __global__ __launch_bounds__(256) void snac_out_kernel(const float* xs, const fl
     audio = io->audio;
     pcm = io->pcm;
   }
-  const int bt = blockIdx.y;
-  const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
-  const int part = threadIdx.x & 3;  // channels part*16 .. part*16+15
-  const float* xb = xs + (size_t)bt * T * 64 + part * 16;  // channels-last [T][64]
-  float acc = 0.f;
-  if (t < T) {
+  __shared__ float4 xt[OUT_T + 6][16];  // rows t0 - 3 .. t0 + OUT_T + 2, 64 channels each
+  const int bt = blockIdx.y, t0 = blockIdx.x * OUT_T;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float4* xb = reinterpret_cast<const float4*>(xs + (size_t)bt * T * 64);
+  // every staging load issued before any is stored (a load -> store loop waits one memory
+  // round trip per iteration)
+  constexpr int NL = ((OUT_T + 6) * 16 + 255) / 256;
+  float4 xv[NL];
+#pragma unroll
+  for (int n = 0; n < NL; ++n) {
+    const int i = tid + 256 * n, r = i >> 4, q = i & 15, tt = t0 - 3 + r;
+    xv[n] = (i < (OUT_T + 6) * 16 && tt >= 0 && tt < T) ? xb[(size_t)tt * 16 + q]
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int n = 0; n < NL; ++n) {
+    const int i = tid + 256 * n;
+    if (i < (OUT_T + 6) * 16) xt[i >> 4][i & 15] = xv[n];
+  }
+  const int j = lane & 15, sub = lane >> 4;  // channel quad j; 4 samples per wave instruction
+  float wk[7][4];
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wk[k][e] = w[(4 * j + e) * 7 + k];
+  const float bias = b[0];
+  __syncthreads();
+  // wave wid: samples t0 + 64 wid + 4 it + sub, it = 0..15
+  for (int it = 0; it < OUT_T / 16; ++it) {
+    const int tl = 64 * wid + 4 * it + sub;  // local sample; its taps are rows tl .. tl + 6
+    float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      const int tt = t + k - 3;
-      if (tt < 0 || tt >= T) continue;
-      const float4* xr = reinterpret_cast<const float4*>(xb + (size_t)tt * 64);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = xr[q];
-        const int ch = part * 16 + 4 * q;
-        acc = fmaf(w[ch * 7 + k], v.x, acc);
-        acc = fmaf(w[(ch + 1) * 7 + k], v.y, acc);
-        acc = fmaf(w[(ch + 2) * 7 + k], v.z, acc);
-        acc = fmaf(w[(ch + 3) * 7 + k], v.w, acc);
-      }
+      const float4 v = xt[tl + k][j];
+      acc = fmaf(wk[k][0], v.x, acc);
+      acc = fmaf(wk[k][1], v.y, acc);
+      acc = fmaf(wk[k][2], v.z, acc);
+      acc = fmaf(wk[k][3], v.w, acc);
     }
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  if (t >= T || part != 0) return;
-  const float v = tanhf(acc + b[0]);
-  if (audio) audio[(size_t)bt * T + t] = v;
-  if (pcm && t >= lo && t < hi) {
-    const float s = v * 32767.0f;
-    pcm[(size_t)bt * (hi - lo) + (t - lo)] = (int16_t)truncf(s);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    acc += __shfl_xor(acc, 8, 64);
+    const int t = t0 + tl;
+    if (j != 0 || t >= T) continue;
+    const float v = tanhf(acc + bias);
+    if (audio) audio[(size_t)bt * T + t] = v;
+    if (pcm && t >= lo && t < hi) {
+      const float s = v * 32767.0f;
+      pcm[(size_t)bt * (hi - lo) + (t - lo)] = (int16_t)truncf(s);
+    }
   }
 }
 
@@ -584,7 +632,7 @@ hipError_t launch_conv_gemm(const ConvGemmArgs& a, int nphase, hipStream_t st) {
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
                            int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
                            const SnacIO* io) {
-  hipLaunchKernelGGL(snac_out_kernel, dim3((T + 63) / 64, B), dim3(256), 0, st, xs, w, b, T, lo,
+  hipLaunchKernelGGL(snac_out_kernel, dim3((T + OUT_T - 1) / OUT_T, B), dim3(256), 0, st, xs, w, b, T, lo,
                      hi, audio, pcm, io);
   return hipGetLastError();
 }
