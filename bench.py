@@ -51,7 +51,12 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(kind, record="r02_pmc_gemv.json"):
+PMC_RECORD = "r03_pmc_gemv.json" if os.path.exists(
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_pmc_gemv.json")) \
+    else "r02_pmc_gemv.json"
+
+
+def pmc_traffic(kind, record=PMC_RECORD):
     """HBM bytes per launch of kernel ``kind`` measured by PMC counters in separate rocprofv3
     passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_gemv.py and
     scripts/gpu_pmc_r03.sh, summarised under profiles/); None when that record is absent."""
@@ -589,7 +594,7 @@ def main():
                          "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
                          "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
                          "traffic": pmc_traffic("gate_up"),
-                         "traffic_source": "profiles/r02_pmc_gemv.json (rocprofv3 --pmc "
+                         "traffic_source": f"profiles/{PMC_RECORD} (rocprofv3 --pmc "
                                            "FETCH_SIZE / WRITE_SIZE, separate passes)"},
             "eager_step_us_by_kernel": per_step_us,
             "gemv_graph_us": {k: {"us": round(v[0], 2), "GB/s": round(v[1] / v[0] / 1e3, 1)}
