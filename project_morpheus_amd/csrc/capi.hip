@@ -135,6 +135,7 @@ struct mx_llm {
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_probe = 0;                // option (diagnostic, results invalid): see GemvArgs
+  int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
@@ -610,6 +611,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
   g.rows_probe = x->rows_probe;
+  g.rows_head_target = x->rows_head_target;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
   g.tickets = x->rows_tickets;
@@ -1129,6 +1131,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_nt_max") {
     if (value != 0 && value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rows_nt_max must be 0, 1, 2 or 4");
     x->rows_nt_max = value;
+  } else if (k == "rows_head_target") {
+    if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_head_target must be 0..4096");
+    x->rows_head_target = value;
   } else if (k == "rows_probe") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_probe must be 0 or 1");
     x->rows_probe = value;

@@ -5,7 +5,7 @@ summaries of scripts/pmc_summary.py over scripts/pmc_gemv.py --rows 1.
 import json
 import sys
 
-KINDS = {"gemv1_kernel<6, 2, 3,": ("qkv", 31457280), "gemv1_kernel<6, 2, 1, false, 8": ("o_proj", 18874368),
+KINDS = {"gemv1_kernel<6, 2, 3,": ("qkv", 31457280), "gemv1_kernel<6, 1, 1, false, 4": ("o_proj", 18874368),
          "gemv1_kernel<6, 2, 2,": ("gate_up", 100663296), "gemv1_kernel<16, 1, 1,": ("down", 50331648)}
 
 

@@ -268,6 +268,17 @@ def test_batched_decode_orpheus_width_64_rows():
     assert _compare_rows(cfg, w, _orpheus_prompts(64, 26, 3, 1), 3) >= 0.8 * 64 * 3
 
 
+@pytest.mark.parametrize("head_target", [2048, 4096])
+def test_batched_lm_head_k_split_orpheus_width(head_target):
+    """The multi-row lm_head split over 2 / 4 K ranges (option rows_head_target): the last
+    arriving range of each vocabulary tile merges the partials and runs the penalty + argmax
+    epilogue (and keeps the logits), 12 rows and prefill at Orpheus widths."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=33)
+    assert _compare_rows(cfg, w, _orpheus_prompts(12, 34, 4, 1), 4,
+                         options={"rows_head_target": head_target}) >= 0.8 * 12 * 4
+
+
 def test_full_depth_orpheus_3b_single_stream():
     """configs[1]'s exact model: all 28 layers at Orpheus-3B widths (6.6 GB of bf16 weights,
     the 156,940-entry tied lm_head), one stream, teacher-forced against the fp32 oracle on
