@@ -274,6 +274,43 @@ __device__ __forceinline__ void conv_gemm_store4(const ConvGemmArgs& a, f32x4 v,
   }
 }
 
+// Epilogue operands gathered before any output is stored.  In the residual units R and out
+// are the same buffer, so the compiler may not move a later element's R (or bias / noise /
+// alpha) load above an earlier element's store: every element of the epilogue paid its own
+// dependent memory round trip.  Loading them all first keeps each element's read-before-write
+// (the elements of a thread are distinct) and the arithmetic of conv_gemm_store(4).
+struct CgOps4 {
+  f32x4 bias, r, a2;
+  float nz;
+};
+__device__ __forceinline__ CgOps4 conv_gemm_ops4(const ConvGemmArgs& a, int m, int n, int ph,
+                                                 int bt) {
+  CgOps4 p;
+  p.bias = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + m) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int col = a.col_stride * n + ph;
+  const size_t o = ((size_t)bt * a.Tout + col) * a.M + m;
+  p.r = (a.epi == CG_RESID || a.epi == CG_NOISE) ? *reinterpret_cast<const f32x4*>(a.R + o)
+                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+  p.nz = a.epi == CG_NOISE ? a.noise[(size_t)bt * a.noise_stride + col] : 0.f;
+  p.a2 = a.out2 ? *reinterpret_cast<const f32x4*>(a.alpha2 + m) : f32x4{0.f, 0.f, 0.f, 0.f};
+  return p;
+}
+__device__ __forceinline__ void conv_gemm_store4p(const ConvGemmArgs& a, f32x4 v, int m, int n,
+                                                  int ph, int bt, const CgOps4& p) {
+  const int col = a.col_stride * n + ph;
+  if (a.bias) v += p.bias;
+  const size_t o = ((size_t)bt * a.Tout + col) * a.M + m;
+  if (a.epi == CG_RESID) v += p.r;
+  else if (a.epi == CG_NOISE) v = p.r + p.nz * v;
+  *reinterpret_cast<f32x4*>(a.out + o) = v;
+  if (a.out2) {
+    f32x4 s2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s2[r] = snake(v[r], p.a2[r]);
+    *reinterpret_cast<f32x4*>(a.out2 + o) = s2;
+  }
+}
+
 template <int WK, int NSUB>
 __global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
   constexpr int BM = 32, BN = 16 * NSUB;
@@ -293,15 +330,41 @@ __global__ __launch_bounds__(WK * 64) void conv_gemm_kernel(ConvGemmArgs a) {
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) red[wk][(16 * i + 4 * g + rg) * BN + 16 * j + c] = acc[i][j][rg];
   __syncthreads();
-  for (int e = threadIdx.x; e < BM * BN; e += WK * 64) {
-    const int nn = e / BM, mm = e - nn * BM;  // consecutive threads: consecutive channels
+  // element e = tid + WK 64 it: consecutive threads take consecutive channels; operands of
+  // every element first, then the stores (see conv_gemm_ops4)
+  constexpr int IT = BM * BN / (WK * 64);
+  static_assert(IT * WK * 64 == BM * BN, "epilogue tiling");
+  float ob[IT], orr[IT], onz[IT], oa2[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = threadIdx.x + WK * 64 * it;
+    const int nn = e / BM, mm = e - nn * BM, m = m0 + mm;
+    const int n = min(n0 + nn, a.Tin - 1);
+    const int col = a.col_stride * n + ph;
+    const size_t o = ((size_t)bt * a.Tout + col) * a.M + m;
+    ob[it] = a.bias ? a.bias[m] : 0.f;
+    orr[it] = (a.epi == CG_RESID || a.epi == CG_NOISE) ? a.R[o] : 0.f;
+    onz[it] = a.epi == CG_NOISE ? a.noise[(size_t)bt * a.noise_stride + col] : 0.f;
+    oa2[it] = a.out2 ? a.alpha2[m] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = threadIdx.x + WK * 64 * it;
+    const int nn = e / BM, mm = e - nn * BM;
     const int n = n0 + nn;
     if (n >= a.Tin) continue;
     const int ei = mm * BN + nn;
     float v = red[0][ei];
 #pragma unroll
     for (int w = 1; w < WK; ++w) v += red[w][ei];
-    conv_gemm_store(a, v, m0 + mm, n, ph, bt);
+    // conv_gemm_store with the gathered operands
+    const int col = a.col_stride * n + ph;
+    if (a.bias) v += ob[it];
+    const size_t o = ((size_t)bt * a.Tout + col) * a.M + m0 + mm;
+    if (a.epi == CG_RESID) v = orr[it] + v;
+    else if (a.epi == CG_NOISE) v = orr[it] + onz[it] * v;
+    a.out[o] = v;
+    if (a.out2) a.out2[o] = snake(v, oa2[it]);
   }
 }
 
@@ -315,13 +378,19 @@ __global__ __launch_bounds__(64) void conv_gemm1_kernel(ConvGemmArgs a) {
   const int ph = blockIdx.z / a.B, bt = blockIdx.z - ph * a.B;
   f32x4 acc[2][NSUB];
   conv_gemm_tile<NSUB>(a, 0, a.nseg * a.Cin, n0, m0, ph, bt, lane, acc);
+  CgOps4 ops[2][NSUB];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j)
+      ops[i][j] = conv_gemm_ops4(a, m0 + 16 * i + 4 * g, min(n0 + 16 * j + c, a.Tin - 1), ph, bt);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NSUB; ++j) {
       const int n = n0 + 16 * j + c;
       if (n >= a.Tin) continue;
-      conv_gemm_store4(a, acc[i][j], m0 + 16 * i + 4 * g, n, ph, bt);
+      conv_gemm_store4p(a, acc[i][j], m0 + 16 * i + 4 * g, n, ph, bt, ops[i][j]);
     }
 }
 
@@ -374,50 +443,56 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
   const bool xin = xcol < ncol;
   const int xbt = xin ? xcol / a.Tin : 0, xt = xin ? xcol - xbt * a.Tin : 0;
   const float* Xw = a.X + (size_t)xbt * a.Tin * a.Cin;
-  uint4 ra[BMT][3];
+  // (native vector types: as HIP's uint4 struct the copies global -> ra -> LDS were lowered
+  // to memcpy and ra lived in scratch memory, a store + reload per k step behind vmcnt waits)
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v ra[BMT][3];
   float4 rx[4];
-  auto gload = [&](int kc) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < BMT; ++r)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        ra[r][p] = *reinterpret_cast<const uint4*>(Arow + (size_t)64 * r * Ktot + p * plane + kc);
-    const int seg = kc >= a.Cin ? 1 : 0;
-    const int t = xt + (seg ? d1 : d0);
-    const bool ok = xin && t >= 0 && t < a.Tin;
-    const float4* xp = reinterpret_cast<const float4*>(
-        Xw + (size_t)min(max(t, 0), a.Tin - 1) * a.Cin + (kc - seg * a.Cin) + 16 * xh);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rx[q] = ok ? xp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  auto lstore = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < BMT; ++r)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) As[p][4 * r + (ar >> 4)][aq * 16 + (ar & 15)] = ra[r][p];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // 8 channels = k group g' = 2 xh + h of column xn
-      float x[8] = {rx[2 * h].x, rx[2 * h].y, rx[2 * h].z, rx[2 * h].w,
-                    rx[2 * h + 1].x, rx[2 * h + 1].y, rx[2 * h + 1].z, rx[2 * h + 1].w};
-      bf16x8 xf[3];
-      rows::split_parts<3>(x, xf);
-      const int gg = 2 * xh + h;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) Bs[p][xn >> 4][gg * 16 + (xn & 15)] = __builtin_bit_cast(uint4, xf[p]);
-    }
-  };
+  bool xok = false;
+  // (macros, not lambdas: with the staging registers captured by reference the compiler kept
+  // ra in scratch memory -- a store and a reload per k step behind a vmcnt wait)
+#define MX_TILED_GLOAD(KC)                                                                     \
+  do {                                                                                         \
+    const int kc_ = (KC);                                                                      \
+    _Pragma("unroll") for (int r = 0; r < BMT; ++r)                                            \
+    _Pragma("unroll") for (int p = 0; p < 3; ++p)                                              \
+      ra[r][p] = *reinterpret_cast<const u32x4v*>(Arow + (size_t)64 * r * Ktot + p * plane + kc_); \
+    const int seg_ = kc_ >= a.Cin ? 1 : 0;                                                     \
+    const int t_ = xt + (seg_ ? d1 : d0);                                                      \
+    xok = xin && t_ >= 0 && t_ < a.Tin;                                                        \
+    /* unconditional loads (the address is clamped in range), zeroed in MX_TILED_LSTORE */     \
+    const float4* xp_ = reinterpret_cast<const float4*>(                                       \
+        Xw + (size_t)min(max(t_, 0), a.Tin - 1) * a.Cin + (kc_ - seg_ * a.Cin) + 16 * xh);     \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) rx[q] = xp_[q];                              \
+  } while (0)
+#define MX_TILED_LSTORE()                                                                      \
+  do {                                                                                         \
+    _Pragma("unroll") for (int r = 0; r < BMT; ++r)                                            \
+    _Pragma("unroll") for (int p = 0; p < 3; ++p)                                              \
+      As[p][4 * r + (ar >> 4)][aq * 16 + (ar & 15)] = __builtin_bit_cast(uint4, ra[r][p]);     \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h) { /* channels 8 (2 xh + h) .. of column xn */ \
+      float x_[8] = {rx[2 * h].x, rx[2 * h].y, rx[2 * h].z, rx[2 * h].w,                       \
+                     rx[2 * h + 1].x, rx[2 * h + 1].y, rx[2 * h + 1].z, rx[2 * h + 1].w};      \
+      _Pragma("unroll") for (int e = 0; e < 8; ++e) x_[e] = xok ? x_[e] : 0.f;                \
+      bf16x8 xf_[3];                                                                           \
+      rows::split_parts<3>(x_, xf_);                                                           \
+      const int gg_ = 2 * xh + h;                                                              \
+      _Pragma("unroll") for (int p = 0; p < 3; ++p)                                            \
+        Bs[p][xn >> 4][gg_ * 16 + (xn & 15)] = __builtin_bit_cast(uint4, xf_[p]);              \
+    }                                                                                          \
+  } while (0)
 
   f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gload(0);
+  MX_TILED_GLOAD(0);
   for (int kc = 0; kc < Ktot; kc += 32) {
     __syncthreads();  // the previous step's fragments are consumed
-    lstore();
+    MX_TILED_LSTORE();
     __syncthreads();
-    if (kc + 32 < Ktot) gload(kc + 32);
+    if (kc + 32 < Ktot) MX_TILED_GLOAD(kc + 32);
     bf16x8 af[2][3];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -445,6 +520,9 @@ __global__ __launch_bounds__(256) void conv_gemm_tiled_kernel(ConvGemmArgs a) {
     for (int i = 0; i < 2; ++i) conv_gemm_store4(a, acc[i][j], m0 + 32 * wm + 16 * i + 4 * g, t, ph, bt);
   }
 }
+
+#undef MX_TILED_GLOAD
+#undef MX_TILED_LSTORE
 
 // fp32 [n] -> three bf16 planes [3][n] (x = p0 + p1 + p2), for the conv-GEMM weights.
 __global__ void split_planes_kernel(const float* src, uint16_t* dst, int64_t n) {
