@@ -588,7 +588,10 @@ static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
   if (x->att_cpw_batch > 0) return x->att_cpw_batch;
   const int nw = x->att_nw_batch;
   const int pairs = R * x->c.kv_heads;
-  const int splits = std::max(1, 256 / pairs);
+  // one split above 64 (row, kv-head) pairs: at 16 rows x 8 kv heads two splits + the ticket
+  // merge took 1.966 ms per fp8 step against 1.846 for one split; at 8 rows the 3-split
+  // choice and one split are equal (1.752 / 1.763 ms; profiles/r03_attn_rows_split_ab.log)
+  const int splits = pairs > 64 ? 1 : std::max(1, 256 / pairs);
   const int chunks = (max_len + 31) / 32;
   return att_cpw_pick((chunks + splits * nw - 1) / (splits * nw), nw);
 }
