@@ -437,12 +437,16 @@ def main():
     from project_morpheus_amd.weights import synthetic_llm_weights, synthetic_snac_weights
 
     cfg = C.OrpheusConfig()
+    free0 = torch.cuda.mem_get_info(local)[0]
     w = synthetic_llm_weights(cfg, seed=0, device=f"cuda:{local}")
     B3 = args.batch
     llm = LlmEngine(cfg, w, device=local, max_slots=max(1, B3), max_pos=2048,
                     max_batch=max(1, B3), max_prefill=512)
     del w
     torch.cuda.empty_cache()
+    # device memory the engine holds (driver view): bf16 weights row-major for the one-row
+    # GEMVs + the fragment-major copies the multi-row GEMMs read, KV cache and workspaces
+    engine_hbm_gb = round((free0 - torch.cuda.mem_get_info(local)[0]) / 1e9, 2)
     snac = SnacDecoder(synthetic_snac_weights(), device=local, max_frames=7,
                        max_batch=max(1, B3))
     syn = Synthesizer(llm, snac, depth=3, seed=rank)
@@ -584,6 +588,7 @@ def main():
             **({"configs_2_no_compaction": batched_nc} if batched_nc else {}),
             "configs_3_long_read": long_read,
             "configs_4_fp8": fp8,
+            "engine_hbm_gb": engine_hbm_gb,
             "decode_step_ms": round(step_ms, 4),
             "decode_step_ms_one_launch_option": round(one_launch_step_ms, 4),
             "decode_tok_per_s": round(1e3 / step_ms, 1),
