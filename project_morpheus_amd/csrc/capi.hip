@@ -1454,15 +1454,13 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
   float* Cs = s->bufC; // Snake(x) for the next ConvTranspose / output conv
   // noise layout per window: [32N | 256N | 1024N | 2048N]
   const int nlen = 3360 * n_frames;
-  const float* nz = noise;
-  if (!nz) {
-    MX_TRY(s, launch_gauss(s->noise, (int64_t)nlen * B, seed, seeds, nlen, st, io));
-    nz = s->noise;
-  }
+  // device-drawn noise (noise == null) is generated by the embed launch below
+  const float* nz = noise ? noise : s->noise;
   const float* cb[3] = {W("q0.codebook"), W("q1.codebook"), W("q2.codebook")};
   const float* pw[3] = {W("q0.out_proj.w"), W("q1.out_proj.w"), W("q2.out_proj.w")};
   const float* pb[3] = {W("q0.out_proj.b"), W("q1.out_proj.b"), W("q2.out_proj.b")};
-  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, A, st, io));    // A: [T][768]
+  MX_TRY(s, launch_snac_embed(frames, n_frames, B, cb, pw, pb, A, st, io,      // A: [T][768]
+                              noise ? nullptr : s->noise, (int64_t)nlen * B, nlen, seed, seeds));
   MX_TRY(s, launch_dwconv(A, Bf, W("in.dw.w"), W("in.dw.b"), nullptr, nullptr, B, 768, T, 1, st));
   {
     ConvGemmArgs g{};
@@ -1520,7 +1518,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
   return MX_OK;
 }
 
-// One window batch.  Device-drawn noise (noise == NULL, the serving path): the ~30 launches
+// One window batch.  Device-drawn noise (noise == NULL, the serving path): the ~35 launches
 // are captured once per (n_frames, batch, slice) into a hipGraph and replayed after a 1-thread
 // kernel stores this call's pointers for the captured kernels to read.  Explicit noise (the
 // parity tests) runs eagerly.

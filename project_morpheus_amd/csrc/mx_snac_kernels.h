@@ -42,7 +42,9 @@ hipError_t launch_set_io(SnacIO* dst, const SnacIO& v, hipStream_t st);
 hipError_t launch_snac_embed(const int32_t* frames, int n_frames, int B,
                              const float* const* codebooks, const float* const* proj_w,
                              const float* const* proj_b, float* z, hipStream_t st,
-                             const SnacIO* io = nullptr);
+                             const SnacIO* io = nullptr, float* noise = nullptr,
+                             int64_t noise_n = 0, int64_t noise_per = 1, uint64_t seed = 0,
+                             const uint64_t* seeds = nullptr);
 hipError_t launch_dwconv(const float* x, float* y, const float* w, const float* b,
                          const float* alpha_in, const float* alpha_out, int B, int C, int T,
                          int dil, hipStream_t st);
@@ -51,7 +53,5 @@ hipError_t launch_split_planes(const float* src, uint16_t* dst, int64_t n, hipSt
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
                            int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
                            const SnacIO* io = nullptr);
-hipError_t launch_gauss(float* out, int64_t n, uint64_t seed, const uint64_t* seeds, int64_t per,
-                        hipStream_t st, const SnacIO* io = nullptr);
 
 }  // namespace mx
