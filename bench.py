@@ -11,6 +11,10 @@ GPU, independent utterances per rank (batch-sharded streams, no data-path collec
 max-over-ranks time, ``scaling: weak``.
 
     python bench.py [--gpus N --steps K --warmup W]
+
+``--gpus N`` without a launcher (no ``WORLD_SIZE`` in the environment) starts the N rank
+processes itself, one per GPU, before anything touches a GPU (``launch_ranks``); under
+``torch.distributed.run`` each rank checks that the world it joined has N ranks.
 """
 from __future__ import annotations
 
@@ -48,7 +52,76 @@ def parse():
                    help="configs[3]: long_read documents (0 skips it)")
     p.add_argument("--step-pos", type=int, default=600,
                    help="position at which the bare decode-step time is measured")
+    p.add_argument("--share-of", type=int, default=8,
+                   help="N = 1: also time configs[3]'s largest per-rank share of an N-GPU "
+                        "run on this GPU (0 skips it)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only: gloo process group, barrier, rank count; no GPU")
     return p.parse_args()
+
+
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` with no launcher: start N copies of this script as rank processes (RANK /
+    LOCAL_RANK = GPU index, WORLD_SIZE = N, rendezvous on 127.0.0.1), wait for all of them and
+    return the worst exit code.  The parent never initialises a GPU (it starts children, it
+    does not exec), and only rank 0 prints the result line."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, pr in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = pr.poll()
+            if any(rc not in (None, 0) for rc in rcs):  # one rank failed: stop the others
+                for i, pr in enumerate(procs):
+                    if rcs[i] is None:
+                        pr.send_signal(signal.SIGTERM)
+                for i, pr in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = pr.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            pr.kill()
+                            rcs[i] = pr.wait()
+                break
+            time.sleep(0.2)
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    bad = [rc for rc in rcs if rc]
+    return max(bad, key=abs) if bad else 0
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """The rank plumbing of a multi-GPU run without the GPU: join a gloo group, barrier, sum
+    one per rank; rank 0 prints the count beside ``n_gpus``."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": seen,
+                          "gpus_flag": args.gpus}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 PMC_RECORD = "r03_pmc_gemv.json" if os.path.exists(
@@ -212,6 +285,15 @@ async def _asgi_speech(app, text: str):
     return t0, marks
 
 
+def _orchestrated(drivers):
+    """The reference server's pull pattern over the adapter (harness/orchestrator_contract.py),
+    collecting each request's driver for its pull count."""
+    import functools
+
+    from harness.orchestrator_contract import orchestrated_pcm_stream
+    return functools.partial(orchestrated_pcm_stream, drivers=drivers)
+
+
 def _http_result(workload, t0, marks, orchs=None):
     pcm = sum(n for _, n in marks) - 44
     wall = marks[-1][0] - t0
@@ -252,7 +334,8 @@ def run_http(args, syn, prompt_text, inject, local, orchestrated=False):
                 yield pcm
 
     orchs = []
-    app = build_app(adapter_cls=BenchAdapter, orchestrated=orchestrated, orchestrators=orchs)
+    app = build_app(adapter_cls=BenchAdapter,
+                    orchestrated_stream=_orchestrated(orchs) if orchestrated else None)
     asyncio.run(_asgi_speech(app, prompt_text))  # warm
     t0, marks = asyncio.run(_asgi_speech(app, prompt_text))
     return _http_result("configs[1] via POST /v1/audio/speech (ASGI app, RIFF + PCM16 stream), "
@@ -279,8 +362,8 @@ def run_http_service(args, llm, snac, cfg, prompt_text):
     old, S._service = S._service, svc
     try:
         orchs = []
-        app = build_app(orchestrators=orchs)
-        asyncio.run(_asgi_speech(app, prompt_text))  # warm (graphs, step kernel)
+        app = build_app(orchestrated_stream=_orchestrated(orchs))
+        asyncio.run(_asgi_speech(app, prompt_text))  # warm (graphs)
         t0, marks = asyncio.run(_asgi_speech(app, prompt_text))
     finally:
         S._service = old
@@ -314,7 +397,7 @@ def run_orchestrator_ceiling(audio_seconds: float, unit: str):
                 yield pcm[i:i + 4096]
 
     orchs = []
-    app = build_app(adapter_cls=Prefilled, orchestrators=orchs)
+    app = build_app(adapter_cls=Prefilled, orchestrated_stream=_orchestrated(orchs))
     asyncio.run(_asgi_speech(app, "Hello world"))
     t0, marks = asyncio.run(_asgi_speech(app, "Hello world"))
     return _http_result(f"orchestrated HTTP path with a pre-filled source ({audio_seconds:.1f} s "
@@ -364,6 +447,27 @@ def run_long_read(args, llm, snac, rank, world, dist):
         return None
     audio = sum(len(v) for v in out.values()) / 24000.0
     mine = S.assign(jobs, world)
+    share = None
+    if world == 1 and args.share_of > 1:
+        # strong-scaling forecast measured on hardware: the most loaded rank of an
+        # args.share_of-GPU run (assign() is deterministic, so this is exactly its job list)
+        # served alone on this GPU
+        plan = S.assign(jobs, args.share_of)
+        r_max = max(range(args.share_of), key=lambda r: (sum(jobs[i].cost for i in plan[r]), -r))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pcm = synthesize([jobs[i] for i in plan[r_max]])
+        torch.cuda.synchronize()
+        t_share = time.perf_counter() - t0
+        ideal = wall / args.share_of
+        share = {"share_of": args.share_of, "rank": r_max, "jobs": len(plan[r_max]),
+                 "wall_s": round(t_share, 3),
+                 "audio_seconds": round(sum(len(p) for p in pcm) / 2 / 24000.0, 2),
+                 "predicted_value": round(audio / t_share, 3),
+                 "predicted_strong_scaling_eff": round(ideal / t_share, 4),
+                 "note": ("the most loaded rank's jobs of an N-GPU run timed alone on one GPU; "
+                          "predicted value = all documents' audio / that wall (the rank-0 "
+                          "gather and stitch excluded)")}
     return {"workload": (f"configs[3]: long_read, {len(docs)} documents x ~3000 chars (seed 5) "
                          f"-> {len(jobs)} <=1000-char batches x {args.max_tokens} tokens, "
                          f"sharded over {world} GPU(s), continuous batching per GPU, ordered "
@@ -372,7 +476,8 @@ def run_long_read(args, llm, snac, rank, world, dist):
             "jobs_per_rank": [len(m) for m in mine],
             "value": round(audio / wall, 3), "unit": "audio-sec/wall-sec",
             "wall_s": round(wall, 3), "audio_seconds": round(audio, 2),
-            "doc_samples_min": int(min(len(v) for v in out.values()))}
+            "doc_samples_min": int(min(len(v) for v in out.values())),
+            **({"rank_share": share} if share else {})}
 
 
 def run_fp8(args, cfg, local, snac, prompt, inject, rank, world, dist):
@@ -417,13 +522,20 @@ def run_fp8(args, cfg, local, snac, prompt, inject, rank, world, dist):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -532,21 +644,6 @@ def main():
     per_step_us = {k: round(1e3 * v / args.profile_steps, 2) for k, v in prof.items()}
     llm.release_row(0, st)
     st.synchronize()
-    # the same step as ONE dataflow launch (option step=1, step_kernels.hip): A/B record
-    llm.set_option("step", 1)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    llm.prefill(0, 0, prompt, 1.1, st)
-    for _ in range(args.step_pos - len(prompt)):
-        llm.decode(1, st)
-    ev0.record(st)
-    for _ in range(50):
-        llm.decode(1, st)
-    ev1.record(st)
-    ev1.synchronize()
-    one_launch_step_ms = ev0.elapsed_time(ev1) / 50
-    llm.release_row(0, st)
-    st.synchronize()
-    llm.set_option("step", 0)
     # pure decode step (graph replay, no SNAC) against the whole-step byte roofline
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n_rep = 50
@@ -590,7 +687,6 @@ def main():
             "configs_4_fp8": fp8,
             "engine_hbm_gb": engine_hbm_gb,
             "decode_step_ms": round(step_ms, 4),
-            "decode_step_ms_one_launch_option": round(one_launch_step_ms, 4),
             "decode_tok_per_s": round(1e3 / step_ms, 1),
             "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),
                               "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4)},

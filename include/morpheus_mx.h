@@ -124,11 +124,6 @@ int mx_llm_release_row(mx_llm* ctx, int row, void* stream);
  * row index in use (replaces nothing in the reference: vLLM's scheduler compacts its batch
  * internally, engine_class.py:114-134).  MX_ERR_STATE if `dst` is live. */
 int mx_llm_move_row(mx_llm* ctx, int dst, int src, void* stream);
-/* Diagnostic (option "step_trace" = 1): the last one-launch step's per-block timeline, 4 u64
- * per block {entry, wait done, end (100 MHz constant clock), role << 32 | layer}; syncs
- * `stream`; returns the block count copied, -1 without a trace. */
-int64_t mx_llm_step_trace(mx_llm* ctx, unsigned long long* host, int64_t max_blocks,
-                          void* stream);
 /* Host view of decode row `row`: *active = 1 while a stream is bound to it (prefill until
  * release), *next_pos = the position its next token takes. */
 int mx_llm_row_state(const mx_llm* ctx, int row, int* active, int* next_pos);

@@ -101,7 +101,10 @@ class LlamaRef:
 
     @torch.no_grad()
     def forward(self, tokens: Sequence[int], slots: Sequence[int],
-                positions: Sequence[int]) -> torch.Tensor:
+                positions: Sequence[int], last_only: bool = False) -> torch.Tensor:
+        """Rows (token, slot, position) through every layer; logits [n, V] (``last_only``:
+        the last row's only, [1, V] -- a prefill needs no more, and at Orpheus width the
+        full [n, 156,940] product dominates a long prompt)."""
         c, w = self.cfg, self.w
         n = len(tokens)
         pos = torch.as_tensor(positions, dtype=torch.int64)
@@ -109,6 +112,11 @@ class LlamaRef:
         h = w["embed"][torch.as_tensor(tokens, dtype=torch.int64)].clone()      # [n,H]
         scale = 1.0 / math.sqrt(c.head_dim)
         group = c.heads // c.kv_heads
+        # rows grouped by slot: each group attends causally over its slot's cache in one
+        # masked product (row i sees positions [0, positions[i]])
+        groups: Dict[int, List[int]] = {}
+        for i, s in enumerate(slots):
+            groups.setdefault(int(s), []).append(i)
         for l in range(c.layers):
             p = f"l{l}."
             xn = _rms(h, w[p + "attn_norm"], c.eps)
@@ -123,18 +131,24 @@ class LlamaRef:
                 kv[l, 0, :, positions[i]] = k[i]
                 kv[l, 1, :, positions[i]] = v[i]
             att = torch.empty(n, c.heads, c.head_dim)
-            for i in range(n):                      # ... then attend causally over [0, pos]
-                kv = self._slot(slots[i])
-                L = positions[i] + 1
+            for s, rows in groups.items():          # ... then attend causally over [0, pos]
+                kv = self._slot(s)
+                ri = torch.as_tensor(rows, dtype=torch.int64)
+                rp = pos[ri]
+                L = int(rp.max()) + 1
                 K = kv[l, 0, :, :L].repeat_interleave(group, dim=0)        # [heads, L, d]
                 V = kv[l, 1, :, :L].repeat_interleave(group, dim=0)
-                s = torch.einsum("hd,hld->hl", q[i], K) * scale
-                att[i] = torch.einsum("hl,hld->hd", torch.softmax(s, dim=-1), V)
+                sc = torch.einsum("rhd,hld->rhl", q[ri], K) * scale
+                mask = torch.arange(L)[None, :] > rp[:, None]              # [r, L]
+                sc = sc.masked_fill(mask[:, None, :], float("-inf"))
+                att[ri] = torch.einsum("rhl,hld->rhd", torch.softmax(sc, dim=-1), V)
             h = h + att.view(n, -1) @ w[p + "wo"].T
             xn = _rms(h, w[p + "mlp_norm"], c.eps)
             g = xn @ w[p + "wg"].T
             u = xn @ w[p + "wu"].T
             h = h + (torch.nn.functional.silu(g) * u) @ w[p + "wd"].T
+        if last_only:
+            h = h[-1:]
         return _rms(h, w["norm"], c.eps) @ w["lm_head"].T                      # [n,V]
 
 
@@ -157,7 +171,8 @@ def greedy_generate(model: LlamaRef, prompt: Sequence[int], n_steps: int,
     can still be compared after a near-tie flipped one argmax."""
     model.free(slot)
     seen = list(prompt)
-    logits = model.forward(list(prompt), [slot] * len(prompt), list(range(len(prompt))))[-1]
+    logits = model.forward(list(prompt), [slot] * len(prompt), list(range(len(prompt))),
+                           last_only=True)[-1]
     out: List[int] = []
     trace = []
     pos = len(prompt)
@@ -175,3 +190,44 @@ def greedy_generate(model: LlamaRef, prompt: Sequence[int], n_steps: int,
         logits = model.forward([nxt], [slot], [pos])[0]
         pos += 1
     return (out, trace) if return_logits else out
+
+
+def teacher_forced_rows(model: LlamaRef, prompts: Sequence[Sequence[int]],
+                        forced: Sequence[Sequence[int]], penalty: float = 1.1,
+                        shared_prefix: int = 0) -> List[List[torch.Tensor]]:
+    """Penalised logits of every step of several streams, each on its own slot and
+    teacher-forced with ``forced[r]`` (the GPU's tokens): the same numbers as
+    ``greedy_generate(..., forced=forced[r], return_logits=True)`` per row, but one
+    ``forward`` per step for all rows (one pass over the lm_head instead of one per row).
+
+    ``shared_prefix`` > 0: every prompt starts with the same ``shared_prefix`` ids; their
+    K/V are computed once on slot 0 and copied to the other slots (the rows' caches are then
+    exactly what separate prefills would write)."""
+    R = len(prompts)
+    for r in range(R):
+        model.free(r)
+    if shared_prefix:
+        pre = list(prompts[0][:shared_prefix])
+        assert all(list(p[:shared_prefix]) == pre for p in prompts)
+        model.forward(pre, [0] * len(pre), list(range(len(pre))), last_only=True)
+        for r in range(1, R):
+            model.cache[r] = model.cache[0].clone()
+    last = []
+    for r, p in enumerate(prompts):
+        tail = list(p[shared_prefix:])
+        assert tail, "each prompt needs at least one id past the shared prefix"
+        last.append(model.forward(tail, [r] * len(tail),
+                                  list(range(shared_prefix, len(p))), last_only=True)[-1])
+    seen = [list(p) for p in prompts]
+    steps = len(forced[0])
+    assert all(len(f) == steps for f in forced)
+    trace: List[List[torch.Tensor]] = [[] for _ in range(R)]
+    logits = torch.stack(last)
+    for k in range(steps):
+        for r in range(R):
+            trace[r].append(apply_penalty(logits[r], seen[r], penalty))
+            seen[r].append(int(forced[r][k]))
+        if k + 1 < steps:
+            logits = model.forward([int(forced[r][k]) for r in range(R)], list(range(R)),
+                                   [len(prompts[r]) + k for r in range(R)])
+    return trace

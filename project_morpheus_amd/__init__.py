@@ -12,9 +12,8 @@ Layout:
   schedule.py     speechpipe token parsing + window schedule (host logic)
   speechpipe.py   drop-in module for Morpheus_Client/tts_engine/speechpipe.py
   adapter.py      MxTTSAdapter + describe/voice_mapper/register for adapter_registry
-  orchestrator.py the reference Orchestrator contract (ladder pulls, per-pull log, stitch)
   completions.py  /v1/completions SSE token stream (remote_backend wire format)
-  server.py       ASGI app: /v1/audio/speech (direct or orchestrated) + /v1/completions
+  server.py       ASGI app: /v1/audio/speech (4096-B pulls or a control-plane stream hook) + /v1/completions
   inference.py    generation params, voices, prompt framing, long-form split/stitch
   stitcher.py     stitch_chunks (orchestrator/stitcher.py contract)
   weights.py      HF / snac state-dict loaders, synthetic weights, fp8 quantisation

@@ -70,7 +70,6 @@ _SIGS = {
                                          C.POINTER(C.c_float)]),
     "mx_llm_release_row": (C.c_int, [_P, C.c_int, _P]),
     "mx_llm_move_row": (C.c_int, [_P, C.c_int, C.c_int, _P]),
-    "mx_llm_step_trace": (C.c_int64, [_P, C.POINTER(C.c_uint64), C.c_int64, _P]),
     "mx_llm_row_state": (C.c_int, [_P, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mx_llm_history": (C.POINTER(C.c_int32), [_P]),
     "mx_llm_debug_logits": (C.c_int, [_P, C.c_int]),

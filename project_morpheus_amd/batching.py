@@ -39,7 +39,7 @@ import threading
 import time
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Callable, Deque, Dict, Iterator, List, Optional, Sequence
+from typing import Callable, Deque, Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -131,6 +131,29 @@ class _Row:
         self.limit = 0       # tokens this row may issue (max_tokens clipped to max_pos)
         self.parked = False  # released on the device (all tokens issued / stopped)
         self.stopped = False
+
+
+def plan_compaction(rows: List[_Row]) -> List[Tuple[int, int]]:
+    """Row compaction plan, applied to ``rows`` in place: while a free row (no stream) sits
+    below the highest row still decoding, that row's stream moves into the lowest free row.
+    Returns the device moves (dst, src) in order (``mx_llm_move_row``).  ``rows[i].idx == i``
+    holds before and after; a stream keeps its KV slot, so host reads by slot are unaffected,
+    and the steps already queued for the old row index run before the move on the stream.
+    Rows that are parked (all tokens issued) or stopped stay where they are: they decode no
+    more steps, so they never set the row class."""
+    moves = []
+    while True:
+        free = [r for r in rows if r.req is None]
+        live = [r for r in rows if r.req is not None and not r.stopped and not r.parked]
+        if not free or not live:
+            return moves
+        lo, hi = free[0], live[-1]
+        if lo.idx > hi.idx:
+            return moves
+        i, j = lo.idx, hi.idx
+        moves.append((i, j))
+        rows[i], rows[j] = hi, lo
+        hi.idx, lo.idx = i, j
 
 
 class _BatchRing:
@@ -451,23 +474,12 @@ class BatchSynthesizer:
             r.req, r.sched, r.stopped, r.parked, r.slot = None, None, False, False, -1
 
         def compact():
-            """Move the highest live row into the lowest free one, so a step runs the row
-            class of the live stream count (a lone stream in row 31 no longer costs a 32-row
-            step; a single stream decodes in row 0 on the one-launch step)."""
+            """Live rows to a prefix (plan_compaction), so a step runs the row class of the
+            live stream count: a lone stream in row 31 no longer costs a 32-row step."""
             if not self.compact:
                 return
-            while True:
-                free = [r for r in rows if r.req is None]
-                live = [r for r in rows if r.req is not None and not r.stopped and not r.parked]
-                if not free or not live:
-                    return
-                lo, hi = free[0], live[-1]
-                if lo.idx > hi.idx:
-                    return
-                llm.move_row(lo.idx, hi.idx, self.stream)
-                i, j = lo.idx, hi.idx
-                rows[i], rows[j] = hi, lo
-                hi.idx, lo.idx = i, j
+            for dst, src in plan_compaction(rows):
+                llm.move_row(dst, src, self.stream)
 
         def announce():
             # a closing stream's windows were all launched when it closed: once no pending

@@ -14,7 +14,6 @@
 #include "../../include/morpheus_mx.h"
 #include "mx_llm_kernels.h"
 #include "mx_snac_kernels.h"
-#include "mx_step.h"
 
 using namespace mx;
 
@@ -134,29 +133,12 @@ struct mx_llm {
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
-  int rows_probe = 0;                // option (diagnostic, results invalid): see GemvArgs
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
   float *attn_norm_all = nullptr, *mlp_norm_all = nullptr;
-  // one-launch B = 1 step (step_kernels.hip): hand-off buffers, counters, status
-  int step = 0;                 // option: 1 = one-launch dataflow step for B = 1 (measured
-                                // 2.57 vs 1.55 ms bf16, profiles/r03_step_kernel_timeline_*),
-                                // 2 = the same roles cut into per-layer launches (step_cuts)
-  int step_cuts = 9;            // option (step = 2): launches start at qkv and gate/up
-  bool step_ok = false;         // shape instantiated and buffers allocated
-  int step_split_max = 0;
-  float *st_hd = nullptr, *st_ho = nullptr, *st_q = nullptr, *st_kn = nullptr, *st_vn = nullptr;
-  float *st_part = nullptr, *st_att = nullptr, *st_act = nullptr;
-  int* st_cnt = nullptr;
-  int* st_status = nullptr;     // device word
-  int* st_status_host = nullptr;  // host-mapped copy (finish block)
-  int* st_status_dev = nullptr;
-  unsigned long long* st_best = nullptr;
-  unsigned long long* st_trace = nullptr;  // option step_trace: per-block timeline (diagnostic)
-  int64_t st_trace_blocks = 0, st_last_blocks = 0;
 
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -290,24 +272,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->samp_top_p, slots);
   A(x->samp_seed, 2 * slots);
   A(x->logits, (size_t)c.max_batch * c.vocab);
-  x->step_ok = step_supported(c.hidden, c.ffn, c.heads, c.kv_heads, f8) &&
-               c.max_pos <= 128 * STEP_SPLIT;
-  if (x->step_ok) {
-    const int QD = c.heads * 128, KV = c.kv_heads * 128;
-    const int grp = c.heads / c.kv_heads;
-    x->step_split_max = (c.max_pos + STEP_SPLIT - 1) / STEP_SPLIT;
-    A(x->st_hd, NL * c.hidden);
-    A(x->st_ho, NL * c.hidden);
-    A(x->st_q, NL * QD);
-    A(x->st_kn, NL * KV);
-    A(x->st_vn, NL * KV);
-    A(x->st_part, NL * c.kv_heads * x->step_split_max * grp * STEP_PART);
-    A(x->st_att, NL * QD);
-    A(x->st_act, NL * c.ffn);
-    A(x->st_cnt, step_counter_ints(c.layers));
-    A(x->st_status, 1);
-    A(x->st_best, STEP_BEST);
-  }
 #undef A
   if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
@@ -335,15 +299,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
   if (e == hipSuccess) e = hipMemset(x->samp_temp, 0, slots * 4);  // greedy everywhere
   if (e == hipSuccess) e = hipMemset(x->samp_seed, 0, slots * 8);
-  if (e == hipSuccess && x->step_ok) {
-    e = hipMemset(x->st_cnt, 0, step_counter_ints(c.layers) * 4);
-    if (e == hipSuccess) e = hipMemset(x->st_status, 0, 4);
-    if (e == hipSuccess) e = hipMemset(x->st_best, 0, STEP_BEST * 8);
-    void *sh = nullptr, *sd = nullptr;
-    if (e == hipSuccess && mx_host_alloc(64, &sh, &sd) != MX_OK) e = hipErrorOutOfMemory;
-    x->st_status_host = (int*)sh;
-    x->st_status_dev = (int*)sd;
-  }
   if (e == hipSuccess) {
     std::vector<float> ones(slots, 1.0f);
     e = hipMemcpy(x->penalty, ones.data(), slots * 4, hipMemcpyHostToDevice);
@@ -613,7 +568,6 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_pw_f8 = x->rows_pw_f8;
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
-  g.rows_probe = x->rows_probe;
   g.rows_head_target = x->rows_head_target;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -839,48 +793,6 @@ static int check_room(mx_llm* x, int n_rows) {
   return MX_OK;
 }
 
-// One-row step as ONE dataflow launch (step_kernels.hip); the sampler and commit follow as
-// their own launches only when the row samples.
-static hipError_t enqueue_step(mx_llm* x, hipStream_t st) {
-  const auto& c = x->c;
-  StepArgs a{};
-  a.wqkv = x->wqkv_all; a.wo = x->wo_all; a.wgu = x->wgu_all; a.wd = x->wd_all; a.lm = x->lm;
-  a.sqkv = x->sqkv_all; a.so = x->so_all; a.sgu = x->sgu_all; a.sd = x->sd_all; a.slm = x->slm;
-  a.attn_norm = x->attn_norm_all; a.mlp_norm = x->mlp_norm_all; a.norm = x->norm;
-  a.embed = x->embed; a.rope_cos = x->rope_cos; a.rope_sin = x->rope_sin;
-  a.kcache = x->kcache; a.vcache = x->vcache; a.kv_layer_elems = x->kv_layer_elems;
-  a.row_slot = x->row_slot; a.row_pos = x->row_pos; a.row_token = x->row_token;
-  a.seen = x->seen; a.hist = x->hist_dev; a.penalty = x->penalty; a.samp_temp = x->samp_temp;
-  a.logits = x->logits; a.logits_all = x->logits_all; a.best = x->best; a.best_sh = x->st_best;
-  a.h = x->h_dec; a.hd = x->st_hd; a.ho = x->st_ho; a.q = x->st_q; a.knew = x->st_kn;
-  a.vnew = x->st_vn; a.part = x->st_part; a.att = x->st_att; a.act = x->st_act;
-  a.cnt = x->st_cnt; a.status = x->st_status; a.status_host = x->st_status_dev;
-  a.H = c.hidden; a.F = c.ffn; a.heads = c.heads; a.kvh = c.kv_heads; a.V = c.vocab;
-  a.layers = c.layers; a.max_pos = c.max_pos; a.split_max = x->step_split_max;
-  a.scratch_slot = c.max_slots; a.eps = c.eps; a.att_scale = 1.0f / sqrtf(128.0f);
-  const int pos = x->row_active[0] ? x->pos_mirror[0] : 0;  // old positions [0, pos)
-  a.nsplit = std::max(1, (pos + STEP_SPLIT - 1) / STEP_SPLIT);
-  const bool sample = x->row_samples[0] != 0;
-  a.commit = sample ? 0 : 1;
-  a.trace = x->st_trace;
-  x->st_last_blocks = step_blocks(a);
-  hipError_t e = x->step == 2 ? launch_step_cut(a, c.wdtype == WT_FP8, x->step_cuts, st)
-                              : launch_step(a, c.wdtype == WT_FP8, st);
-  if (e != hipSuccess || !sample) return e;
-  SampleArgs sa{};
-  sa.logits = x->logits; sa.row_slot = x->row_slot; sa.row_pos = x->row_pos;
-  sa.temp = x->samp_temp; sa.top_p = x->samp_top_p; sa.seed = x->samp_seed; sa.best = x->best;
-  sa.V = c.vocab;
-  e = launch_sample(sa, 1, st);
-  if (e != hipSuccess) return e;
-  CommitArgs cm{};
-  cm.best = x->best; cm.row_slot = x->row_slot; cm.row_pos = x->row_pos;
-  cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
-  cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
-  cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
-  return launch_commit(cm, 1, st);
-}
-
 extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (!x) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
@@ -888,14 +800,6 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (x->step_ok && x->st_status_host && *reinterpret_cast<volatile int*>(x->st_status_host))
-    MX_FAIL(x, MX_ERR_HIP, "a one-launch decode step gave up waiting (status " +
-                               std::to_string(*x->st_status_host) + "): results invalid");
-  if (n_rows == 1 && x->step && x->step_ok && !x->legacy_gemv) {
-    MX_TRY(x, enqueue_step(x, st));
-    mirror_step(x, 1);
-    return MX_OK;
-  }
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
   const int ml = decode_max_len(x, n_rows);
@@ -1089,24 +993,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
-  } else if (k == "step") {
-    if (value < 0 || value > 2) MX_FAIL(x, MX_ERR_ARG, "step must be 0, 1 or 2");
-    x->step = value;
-  } else if (k == "step_cuts") {  // step = 2: stage starts that begin a launch (mx_step.h)
-    if (value < 1 || value > 31 || !(value & 1)) MX_FAIL(x, MX_ERR_ARG, "step_cuts: 5-bit mask with bit 0 set");
-    x->step_cuts = value;
-  } else if (k == "step_trace") {  // diagnostic: per-block timeline of one-launch steps
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "step_trace must be 0 or 1");
-    if (value && !x->st_trace && x->step_ok) {
-      StepArgs g{};
-      g.H = x->c.hidden; g.F = x->c.ffn; g.heads = x->c.heads; g.kvh = x->c.kv_heads;
-      g.V = x->c.vocab; g.layers = x->c.layers; g.nsplit = x->step_split_max;
-      x->st_trace_blocks = step_blocks(g);
-      MX_TRY(x, hipSetDevice(x->device));
-      MX_TRY(x, x->alloc(&x->st_trace, (size_t)x->st_trace_blocks * 4));
-      MX_TRY(x, hipMemset(x->st_trace, 0, (size_t)x->st_trace_blocks * 32));
-    }
-    if (!value) x->st_trace = nullptr;  // (the buffer stays allocated until destroy)
   } else if (k == "rows_frag") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
     x->rows_frag = value;
@@ -1137,9 +1023,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_head_target must be 0..4096");
     x->rows_head_target = value;
-  } else if (k == "rows_probe") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_probe must be 0 or 1");
-    x->rows_probe = value;
   } else if (k == "rows_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;
@@ -1189,15 +1072,6 @@ extern "C" int mx_llm_move_row(mx_llm* x, int dst, int src, void* stream) {
 
 // Diagnostic: copy the last one-launch step's per-block timeline (4 u64 per block: entry,
 // wait done, end on the 100 MHz constant clock, role << 32 | layer) after syncing `stream`.
-extern "C" int64_t mx_llm_step_trace(mx_llm* x, unsigned long long* host, int64_t max_blocks,
-                                     void* stream) {
-  if (!x || !host || !x->st_trace) return -1;
-  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
-  const int64_t n = std::min(max_blocks, x->st_last_blocks);
-  if (hipMemcpy(host, x->st_trace, (size_t)n * 32, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return n;
-}
-
 extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next_pos) {
   if (!x || !active || !next_pos || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
   *active = x->row_active[row];
@@ -1235,7 +1109,6 @@ extern "C" void mx_llm_destroy(mx_llm* x) {
   if (x->cap) (void)hipStreamDestroy(x->cap);
   for (void* p : x->allocs) (void)hipFree(p);
   if (x->hist_host) (void)hipHostFree(x->hist_host);
-  if (x->st_status_host) (void)hipHostFree(x->st_status_host);
   delete x;
 }
 

@@ -40,7 +40,6 @@ struct GemvArgs {
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
-  int rows_probe;          // diagnostic (results invalid): 1 = K ranges publish partials and exit
                            // (no ticket, no merge, no epilogue): prices the split-K seam
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]

@@ -17,6 +17,7 @@ import itertools
 import multiprocessing as mp
 import queue
 import threading
+import time
 from typing import Callable, Dict, Iterator, List, Optional
 
 from . import inference as I
@@ -28,8 +29,12 @@ def _service_factory(device: int):
     return Service(device=device, max_pos=min(C.MX_MAX_POS, 8192))
 
 
-def _worker(device: int, inbox, outbox, factory: Callable) -> None:
-    """Worker process: one Service on `device`; forwards each stream's chunks to rank 0."""
+def _worker(device: int, inbox, outbox, factory: Callable, content_seed: int = 0) -> None:
+    """Worker process: one Service on `device`; forwards each stream's chunks to rank 0.
+    ``content_seed``: the parent's ``config.CONTENT_SEED`` (a spawn child re-imports config
+    from the environment, so a value the parent set in-process would otherwise be lost)."""
+    from . import config
+    config.CONTENT_SEED = content_seed
     try:
         svc = factory(device)
     except BaseException as e:  # report and exit: the pool marks this worker dead
@@ -112,6 +117,11 @@ class PoolHandle:
         self.pool._cancel(self)
 
 
+def _content_seed() -> int:
+    from . import config
+    return int(config.CONTENT_SEED)
+
+
 class GpuPool:
     def __init__(self, n_workers: int, factory: Callable = _service_factory,
                  devices: Optional[List[int]] = None, start_timeout: float = 600.0,
@@ -122,7 +132,8 @@ class GpuPool:
         self.devices = devices if devices is not None else list(range(n_workers))
         self.inboxes = [ctx.Queue() for _ in self.devices]
         self.outbox = ctx.Queue()
-        self.procs = [ctx.Process(target=_worker, args=(d, ib, self.outbox, factory),
+        self.procs = [ctx.Process(target=_worker, args=(d, ib, self.outbox, factory,
+                                                          _content_seed()),
                                   daemon=True) for d, ib in zip(self.devices, self.inboxes)]
         for p in self.procs:
             p.start()
@@ -143,11 +154,18 @@ class GpuPool:
         self._reader.start()
 
     def _read(self) -> None:
+        # liveness is checked on a clock, not only when the outbox goes quiet: while other
+        # workers stream chunks the outbox never empties, and a dead worker's clients would
+        # otherwise wait forever
+        next_reap = time.monotonic() + self.poll_s
         while True:
-            try:
-                kind, rid, payload = self.outbox.get(timeout=self.poll_s)
-            except queue.Empty:
+            now = time.monotonic()
+            if now >= next_reap:
                 self._reap()
+                next_reap = now + self.poll_s
+            try:
+                kind, rid, payload = self.outbox.get(timeout=max(0.0, next_reap - now))
+            except queue.Empty:
                 continue
             except (EOFError, OSError):
                 return
@@ -195,7 +213,8 @@ class GpuPool:
         ctx = mp.get_context("spawn")
         self.inboxes[w] = ctx.Queue()
         self.procs[w] = ctx.Process(target=_worker, args=(self.devices[w], self.inboxes[w],
-                                                          self.outbox, self.factory), daemon=True)
+                                                          self.outbox, self.factory,
+                                                          _content_seed()), daemon=True)
         self.procs[w].start()
         self._respawned[w] = True
 

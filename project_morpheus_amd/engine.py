@@ -135,16 +135,6 @@ class LlmEngine:
                                                 C.c_void_p(stream.cuda_stream)))
         return out
 
-    def step_trace(self, stream, max_blocks: int = 1 << 20) -> np.ndarray:
-        """Diagnostic (after ``set_option("step_trace", 1)``): the last one-launch step's
-        per-block timeline, uint64 [blocks][4] = entry, wait done, end (100 MHz), role<<32|layer."""
-        buf = np.zeros((max_blocks, 4), dtype=np.uint64)
-        n = self.lib.mx_llm_step_trace(self.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                       max_blocks, C.c_void_p(stream.cuda_stream))
-        if n < 0:
-            raise _lib.MxError("no step trace (enable option step_trace, B = 1 step)")
-        return buf[:n]
-
     def row_state(self, row: int):
         """(active, next position) of decode row ``row`` (host view)."""
         a, p = C.c_int(0), C.c_int(0)

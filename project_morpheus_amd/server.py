@@ -3,13 +3,15 @@
 Restates the reference routes (Morpheus_Client/server.py:50-87 RIFF header + raw PCM16 frames,
 :127-158 ``orchestrated_pcm_stream``, :161-190 ``SpeechRequest`` / ``create_speech_api``,
 :209-222 ``tts_ws``, :236-239 ``/adapters``, :243-289 adapter / voice selection by
-``POST /config``) for the MI355X adapter.  As in the reference, BOTH speech routes run the
-orchestrated stream: an ``Orchestrator`` pulling ``ChunkLadder`` byte windows from the adapter,
-the per-pull structured log, ``stitch_chunks`` (overlap 0) and the WAV streamer
-(orchestrator.py).  ``orchestrated=False`` drains the adapter with 4096-byte pulls instead (one
-SNAC window per pull; a bench comparison, not the reference behaviour).  Pinned to the
-reference server's own bytes by tests/test_server_golden.py (golden made by importing
-``Morpheus_Client.server`` with this adapter registered, tests/golden/make_server_golden.py).
+``POST /config``) for the MI355X adapter.  The reference runs BOTH speech routes through its
+control plane's Orchestrator (server.py:127-158), which this package does not restate
+(reused as-is above the adapter).  ``orchestrated_stream`` is that hook: a
+callable ``adapter -> async iterator of PCM bytes`` (the reference's orchestrated stream in a
+deployment, ``harness.orchestrator_contract.orchestrated_pcm_stream`` in the bench and the
+tests); without it the routes drain the adapter with 4096-byte pulls (one SNAC window each).
+With the harness driver the routes are pinned to the reference server's own bytes by
+tests/test_server_golden.py (golden made by importing ``Morpheus_Client.server`` with this
+adapter registered, tests/golden/make_server_golden.py).
 
 Out of scope (control plane): text sources, ``/stats``, barge-in routes, the
 admin UI and ``.env`` persistence of ``/config``.
@@ -75,14 +77,14 @@ def _service_tokens(prompt_ids, **params):
 
 
 def build_app(adapter_cls=None, token_source=_service_tokens, encode=None,
-              decode=None, orchestrated: bool = True, orchestrators=None,
+              decode=None, orchestrated_stream=None,
               registry: Optional[AdapterRegistry] = None) -> Starlette:
     """``adapter_cls`` (tests / bench): the class registered as ``mi355x`` (default
     ``MxTTSAdapter``).  ``token_source(prompt_ids, **params)`` backs /v1/completions (default:
     this GPU's service); ``encode`` / ``decode`` default to the process tokenizer.
-    ``orchestrators`` collects each request's Orchestrator (pull counts for the bench)."""
+    ``orchestrated_stream(adapter)``: the control plane's PCM stream over an adapter (module
+    docstring); None = plain 4096-byte pulls."""
     from .completions import build_route
-    from .orchestrator import orchestrated_pcm_stream
     from .tokenizer import default_tokenizer
     if encode is None:
         encode = lambda s: default_tokenizer().encode(s)  # noqa: E731
@@ -96,8 +98,8 @@ def build_app(adapter_cls=None, token_source=_service_tokens, encode=None,
         return registry.create(state["adapter"], prompt=prompt, voice=schema, **kw)
 
     def pcm_stream(adapter):
-        if orchestrated:
-            return orchestrated_pcm_stream(adapter, orchestrators)
+        if orchestrated_stream is not None:
+            return orchestrated_stream(adapter)
         return adapter_pcm(adapter)
 
     async def speech(request: Request) -> StreamingResponse:

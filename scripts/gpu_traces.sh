@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-3 GPU session: parity tests, then B=1 step kernel traces (bf16, fp8) with gaps.
+# GPU session: parity tests, smoke, then B=1 decode-step kernel traces (bf16, fp8) with gaps.
 # Each GPU step has its own limit; a fault / abort / timeout ends the script.
 set -u
-OUT=${OUT:-gpurun_out/r03}
+OUT=${OUT:-gpurun_out/traces}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }

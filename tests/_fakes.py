@@ -52,7 +52,11 @@ class FakeService:
 
 
     def submit_tokens(self, prompt_ids, max_tokens=None, **kw):
-        """Token ids: the prompt ids echoed with the device added, max_tokens of them."""
+        """Token ids: the prompt ids echoed with the device added, max_tokens of them
+        (prompt [-1]: the worker's config.CONTENT_SEED, for the seed-propagation test)."""
+        if list(prompt_ids) == [-1]:
+            from project_morpheus_amd import config
+            return FakeHandle([int(config.CONTENT_SEED)])
         n = max_tokens or 8
         toks = [(int(prompt_ids[i % len(prompt_ids)]) + self.device) for i in range(n)]
         return FakeHandle(toks)

@@ -88,3 +88,37 @@ def test_dead_worker_fails_its_streams_and_is_replaced():
         assert list(g.chunks()) == fake_pcm("after", g.worker, 1)
     finally:
         p.close()
+
+
+def test_dead_worker_is_reaped_while_another_streams():
+    """The outbox never goes quiet while a live worker streams chunks every 20 ms; the dead
+    worker's client must still get its error (liveness is checked on a clock)."""
+    p = GpuPool(2, factory=fake_factory, start_timeout=120, poll_s=0.5, respawn=False)
+    try:
+        h = p.submit("die soon", "tara", max_tokens=7000)
+        busy = p.submit("slow busy", "tara", max_tokens=70000)   # 10,000 chunks, 20 ms apart
+        assert (h.worker, busy.worker) == (0, 1)
+        t0 = time.time()
+        with pytest.raises(RuntimeError, match="died"):
+            while h.get(timeout=60) is not None:
+                pass
+        assert time.time() - t0 < 15
+        assert busy.get(timeout=30) is not None   # the other stream is still live
+        busy.cancel()
+        while busy.get(timeout=30) is not None:
+            pass
+    finally:
+        p.close()
+
+
+def test_workers_inherit_the_parents_content_seed(monkeypatch):
+    """MORPHEUS_MX_CONTENT_SEED set in-process (as the parity tests do) reaches spawned
+    workers, which re-import config from the environment."""
+    from project_morpheus_amd import config as C
+    monkeypatch.setattr(C, "CONTENT_SEED", 1)
+    p = GpuPool(1, factory=fake_factory, start_timeout=120)
+    try:
+        h = p.submit_tokens([-1], max_tokens=1)
+        assert h.get(timeout=30) == 1
+    finally:
+        p.close()

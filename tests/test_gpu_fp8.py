@@ -14,6 +14,8 @@ from project_morpheus_amd import config as C
 from project_morpheus_amd.weights import (dequantize_fp8, quantize_fp8,
                                           synthetic_llm_weights)
 
+from _parity import LONG_SHAPES, b1_attention_shapes, check_tokens
+
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 5e-3
@@ -24,11 +26,11 @@ def _cfg():
     return C.OrpheusConfig(hidden=1024, layers=2, heads=8, kv_heads=2, ffn=2048, vocab=1000)
 
 
-def _run(cfg, qw, prompts, steps, info=None, options=None):
+def _run(cfg, qw, prompts, steps, info=None, options=None, max_pos=512, max_prefill=128):
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
-    eng = LlmEngine(cfg, qw, device=0, max_slots=B, max_pos=512, max_batch=B, max_prefill=128,
-                    wdtype="fp8")
+    eng = LlmEngine(cfg, qw, device=0, max_slots=B, max_pos=max_pos, max_batch=B,
+                    max_prefill=max_prefill, wdtype="fp8")
     for k, v in (options or {}).items():
         eng.set_option(k, v)
     eng.enable_logits()
@@ -48,11 +50,12 @@ def _run(cfg, qw, prompts, steps, info=None, options=None):
     return toks, logits
 
 
-def _check(cfg, qw, prompts, steps, info=None, options=None):
-    toks, logits = _run(cfg, qw, prompts, steps, info=info, options=options)
+def _check(cfg, qw, prompts, steps, info=None, options=None, max_pos=512, max_prefill=128):
+    toks, logits = _run(cfg, qw, prompts, steps, info=info, options=options, max_pos=max_pos,
+                        max_prefill=max_prefill)
     rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
                      kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
-    ref = L.LlamaRef(rc, dequantize_fp8(qw), max_pos=512)
+    ref = L.LlamaRef(rc, dequantize_fp8(qw), max_pos=max_pos)
     agree = 0
     for r, p in enumerate(prompts):
         _, rl = L.greedy_generate(ref, p, steps, 1.1, return_logits=True, forced=toks[r])
@@ -60,11 +63,8 @@ def _check(cfg, qw, prompts, steps, info=None, options=None):
             o = rl[k].numpy()
             np.testing.assert_allclose(logits[r][k], o, atol=LOGIT_TOL, rtol=LOGIT_TOL,
                                        err_msg=f"row {r} step {k}")
-            if toks[r][k] != int(np.argmax(o)):
-                top2 = np.sort(o)[-2:]
-                assert top2[1] - top2[0] < TIE_MARGIN
-            else:
-                agree += 1
+            assert toks[r][k] == int(np.argmax(logits[r][k]))
+        agree += check_tokens(toks[r], rl, TIE_MARGIN, what=f"row {r}")
     return agree
 
 
@@ -104,3 +104,26 @@ def test_fp8_batched_orpheus_width_8_rows():
     rng = np.random.default_rng(15)
     prompts = [[int(x) for x in rng.integers(1000, 128000, 5 + 4 * i)] for i in range(8)]
     assert _check(cfg, qw, prompts, 6) >= 0.8 * 8 * 6
+
+
+def test_fp8_single_stream_long_context():
+    """The default fp8 one-row path over configs[1]'s context range (L 200 -> 1,260): the fp8
+    merging o-proj at NSM 2 / 4 / 8 and the 256-position attention past 1,024."""
+    cfg = _cfg()
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=55, std=0.05, norm_jitter=0.5), cfg)
+    prompt = [int(x) for x in np.random.default_rng(16).integers(0, cfg.vocab, 200)]
+    steps = 1060
+    assert LONG_SHAPES <= b1_attention_shapes(201, 200 + steps)
+    assert _check(cfg, qw, [prompt], steps, max_pos=1280, max_prefill=256) >= 0.6 * steps
+
+
+def test_fp8_single_stream_orpheus_width_long_context():
+    """configs[4]'s one-row instantiations at Orpheus widths (the KCH = 3 fp8 merging o-proj
+    gemv1<3,2,1,false,8,true,NSM>) at L 600 -> 1,120, teacher-forced (2 layers, 16,384-entry
+    vocabulary: see test_gpu_llm.test_long_context_orpheus_width_default_path)."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=56), cfg)
+    prompt = [int(x) for x in np.random.default_rng(17).integers(0, cfg.vocab, 600)]
+    steps = 520
+    assert LONG_SHAPES <= b1_attention_shapes(601, 600 + steps)
+    assert _check(cfg, qw, [prompt], steps, max_pos=1152, max_prefill=640) >= 0.7 * steps

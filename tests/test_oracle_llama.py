@@ -88,3 +88,32 @@ def test_param_count_orpheus():
     cfg = C.OrpheusConfig()
     assert cfg.params() == 3_300_691_968
     assert cfg.kv_bytes_per_position() == 114_688
+
+
+def test_teacher_forced_rows_match_per_row_generation():
+    """The batched teacher-forced oracle (one forward per step for all rows, optional shared
+    prefix computed once) gives each row the logits of its own greedy_generate run."""
+    d = small_cfg()
+    pc = C.OrpheusConfig(hidden=d["hidden"], layers=d["layers"], heads=d["heads"],
+                         kv_heads=d["kv_heads"], head_dim=d["head_dim"], ffn=d["ffn"],
+                         vocab=d["vocab"])
+    w = synthetic_llm_weights(pc, seed=9, std=0.05, norm_jitter=0.5)
+    rc = L.RefConfig(hidden=d["hidden"], layers=d["layers"], heads=d["heads"],
+                     kv_heads=d["kv_heads"], head_dim=d["head_dim"], ffn=d["ffn"],
+                     vocab=d["vocab"])
+    rng = np.random.default_rng(3)
+    prefix = [int(x) for x in rng.integers(0, d["vocab"], 20)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, d["vocab"], 2 + 3 * r)]
+               for r in range(4)]
+    forced = [[int(x) for x in rng.integers(0, d["vocab"], 7)] for _ in prompts]
+    # fp32 KV here: the products' summation order differs between one-row and batched
+    # forwards, and with the bf16 KV cache a last-ulp difference can flip a rounding
+    # (1e-4 here, the effect the GPU tests' 5e-3 absorbs)
+    for shared in (0, 20):
+        ref = L.LlamaRef(rc, w, max_pos=128, round_kv=False)
+        got = L.teacher_forced_rows(ref, prompts, forced, 1.1, shared_prefix=shared)
+        for r, p in enumerate(prompts):
+            one = L.LlamaRef(rc, w, max_pos=128, round_kv=False)
+            _, want = L.greedy_generate(one, p, 7, 1.1, return_logits=True, forced=forced[r])
+            for k in range(7):
+                assert torch.allclose(got[r][k], want[k], atol=1e-5, rtol=1e-5), (shared, r, k, float((got[r][k] - want[k]).abs().max()))

@@ -1,14 +1,15 @@
-"""The restated Orchestrator contract (project_morpheus_amd/orchestrator.py) on CPU: the
-ladder starts at 8 and steps by buffer depth (chunk_ladder.py:10-60), every pull is logged
-with its base64 PCM (core.py:97-104), PCM arrives intact through stitch_chunks and the WAV
-streamer, and barge-in resets the adapter."""
+"""The reference server's pull pattern (harness/orchestrator_contract.py, the bench / test
+driver) on CPU: the ladder starts at 8 and steps by buffer depth (chunk_ladder.py:10-60),
+every pull is logged with its base64 PCM (core.py:97-104), PCM arrives intact through
+stitch_chunks and the WAV streamer, and barge-in resets the adapter."""
 import asyncio
 import base64
+import functools
 
 from starlette.testclient import TestClient
 
+from harness.orchestrator_contract import PullDriver, next_rung, orchestrated_pcm_stream
 from project_morpheus_amd.adapter import MxTTSAdapter
-from project_morpheus_amd.orchestrator import ChunkLadder, Orchestrator, PlaybackBuffer
 from project_morpheus_amd.server import build_app, riff_header
 
 PCM = [bytes(range(256)) * 8, b"", bytes(range(100)), bytes(range(200)) * 3]
@@ -21,21 +22,26 @@ class Fake(MxTTSAdapter):
 
 
 def test_ladder_adapt():
-    lad = ChunkLadder()
-    assert lad.current == 8
-    lad.adapt(10.0, (50.0, 250.0))
-    assert lad.current == 12
-    lad.adapt(300.0, (50.0, 250.0))
-    assert lad.current == 8
-    lad.adapt(300.0, (50.0, 250.0))
-    assert lad.current == 8
+    d = PullDriver(None)
+    assert d.window == 8
+    d.rung = next_rung(d.rung, 10.0)
+    assert d.window == 12
+    d.rung = next_rung(d.rung, 300.0)
+    assert d.window == 8
+    d.rung = next_rung(d.rung, 300.0)
+    assert d.window == 8
+    for _ in range(10):
+        d.rung = next_rung(d.rung, 0.0)
+    assert d.window == 64
+    d.rung = next_rung(d.rung, 100.0)   # inside the comfort band: stays
+    assert d.window == 64
 
 
 def test_orchestrator_pulls_log_and_pcm():
     events = []
 
     async def go():
-        o = Orchestrator(Fake("x"), PlaybackBuffer(1000))
+        o = PullDriver(Fake("x"))
         out = [c async for c in o.stream(on_event=events.append)]
         return o, out
 
@@ -57,7 +63,7 @@ def test_barge_in_resets_adapter():
             await super().reset()
 
     async def go():
-        o = Orchestrator(Counting("x"), PlaybackBuffer(1000))
+        o = PullDriver(Counting("x"))
         n = 0
         async for _ in o.stream():
             n += 1
@@ -71,7 +77,8 @@ def test_barge_in_resets_adapter():
 
 def test_orchestrated_speech_route():
     orchs = []
-    app = build_app(adapter_cls=Fake, orchestrated=True, orchestrators=orchs)
+    app = build_app(adapter_cls=Fake, orchestrated_stream=functools.partial(
+        orchestrated_pcm_stream, drivers=orchs))
     r = TestClient(app).post("/v1/audio/speech", json={"input": "Hello", "voice": "tara"})
     assert r.status_code == 200
     assert r.content == riff_header() + b"".join(PCM)
@@ -83,7 +90,7 @@ def test_ms_pull_unit_option():
     what the adapter descriptor declares (adapter_registry.py:54); default stays bytes."""
     async def go(unit):
         a = Fake("x", pull_unit=unit)
-        o = Orchestrator(a, PlaybackBuffer(1000))
+        o = PullDriver(a)
         out = [c async for c in o.stream()]
         return o.pulls, b"".join(c.pcm for c in out), [len(c.pcm) for c in out]
 
