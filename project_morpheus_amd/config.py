@@ -126,6 +126,10 @@ SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
 # "regenerate" gives new audio; 1 derives it from the prompt ids (reproducible bench / parity
 # runs: the same text gives the same audio whatever the batch company or arrival order).
 CONTENT_SEED = env_int("MORPHEUS_MX_CONTENT_SEED", 0)
+# mx_llm_set_option knobs applied to every LlmEngine at creation: MORPHEUS_MX_OPT_<key>=<int>
+# (A/B runs and parity sweeps of a non-default kernel choice, e.g. MORPHEUS_MX_OPT_rows_gen=5).
+ENGINE_OPTIONS = {k[len("MORPHEUS_MX_OPT_"):]: int(v) for k, v in os.environ.items()
+                  if k.startswith("MORPHEUS_MX_OPT_")}
 # Unit of MxTTSAdapter.pull(n): "bytes" (default; the reference adapters slice bytes,
 # llama_local.py:131-150, pinned by tests/test_tts_adapter_chunking.py) or "ms" (what the
 # adapter descriptor declares, adapter_registry.py:54: n milliseconds of PCM = 48 n bytes).

@@ -1,0 +1,19 @@
+// Multi-row decode GEMM generation 5, EPI_SILU instantiations (own translation unit).
+#include "mx_rows_v5.inc"
+
+namespace mx {
+namespace v5 {
+
+// gate/up: 64 weight rows per block (256 blocks at Orpheus width), 32 above 32 batch rows (16
+// with e4m3 weights, whose 64-k load units hold twice the activations)
+// (the cross-wave reduction tile stays within 64 KB of LDS)
+hipError_t launch_rows5_silu(const GemvArgs& a, int nt, hipStream_t st) {
+  const int wpb = a.rows5_wpb ? a.rows5_wpb : 8;
+  if (nt == 1) return launch5<4, 1, EPI_SILU, true>(a, wpb, st);
+  if (nt == 2) return launch5<4, 2, EPI_SILU, true>(a, wpb, st);
+  if (a.wdtype == WT_FP8) return launch5<1, 4, EPI_SILU, true>(a, wpb, st);
+  return launch5<2, 4, EPI_SILU, true>(a, wpb, st);
+}
+
+}  // namespace v5
+}  // namespace mx

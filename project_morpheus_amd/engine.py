@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import STOP_IDS, OrpheusConfig, rope_tables
+from .config import ENGINE_OPTIONS, STOP_IDS, OrpheusConfig, rope_tables
 from .schedule import WindowScheduler, code_of_id
 
 SAMPLES_PER_FRAME = 2048
@@ -72,6 +72,8 @@ class LlmEngine:
         cos, sin = rope_tables(cfg, max_pos)
         self._check(self.lib.mx_llm_set_rope(h, cos.ctypes.data, sin.ctypes.data, max_pos))
         self._check(self.lib.mx_llm_finalize(h))
+        for key, val in ENGINE_OPTIONS.items():   # MORPHEUS_MX_OPT_<key>=<int> overrides
+            self.set_option(key, val)
         hp = self.lib.mx_llm_history(h)
         n = (max_slots + 1) * max_pos
         self.hist = np.ctypeslib.as_array(hp, shape=(n,)).reshape(max_slots + 1, max_pos)
