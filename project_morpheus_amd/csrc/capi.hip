@@ -134,13 +134,6 @@ struct mx_llm {
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
-  int rows_gen = 4;                  // option: multi-row decode GEMM generation (4 or 5)
-  int rows5_wpb = 0;                 // option: generation-5 waves per block (0 = default)
-  int head_gemv1 = 0;                // option: one-row lm_head on gemv1 (load-first) kernels
-  int att_fuse = 0;                  // option: one-row attention + o-proj in one launch
-  int* fuse_cnt = nullptr;           // per layer (32 ints apart): fused-launch arrivals
-  int* fuse_status_host = nullptr;   // host-mapped give-up word of the fused launch
-  int* fuse_status_dev = nullptr;
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
@@ -279,7 +272,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->samp_top_p, slots);
   A(x->samp_seed, 2 * slots);
   A(x->logits, (size_t)c.max_batch * c.vocab);
-  A(x->fuse_cnt, (size_t)c.layers * 32);
 #undef A
   if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
@@ -307,13 +299,6 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
   if (e == hipSuccess) e = hipMemset(x->samp_temp, 0, slots * 4);  // greedy everywhere
   if (e == hipSuccess) e = hipMemset(x->samp_seed, 0, slots * 8);
-  if (e == hipSuccess) e = hipMemset(x->fuse_cnt, 0, (size_t)c.layers * 32 * 4);
-  if (e == hipSuccess) {
-    void *sh = nullptr, *sd = nullptr;
-    if (mx_host_alloc(64, &sh, &sd) != MX_OK) e = hipErrorOutOfMemory;
-    x->fuse_status_host = (int*)sh;
-    x->fuse_status_dev = (int*)sd;
-  }
   if (e == hipSuccess) {
     std::vector<float> ones(slots, 1.0f);
     e = hipMemcpy(x->penalty, ones.data(), slots * 4, hipMemcpyHostToDevice);
@@ -584,9 +569,6 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
   g.rows_head_target = x->rows_head_target;
-  g.rows_gen = x->rows_gen;
-  g.rows5_wpb = x->rows5_wpb;
-  g.head_gemv1 = x->head_gemv1;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
   g.tickets = x->rows_tickets;
@@ -625,9 +607,6 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // QKV + RoPE + KV append
     g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = qkv_rows; g.K = H; g.X = rs.h; g.xstride = H; g.norm_w = l.attn_norm;
     if (x->rows_frag) g.Wf = l.wqkv_f;
-    const bool fuse = rs.R == 1 && !x->legacy_gemv && x->o_merge && x->att_fuse &&
-                      rs.nsplit <= 8 && rs.nw == (x->att_fuse >= 3 ? 8 : 4) && rs.cpw <= 2;
-    if (fuse) g.zero_word = x->fuse_cnt + (size_t)li * 32;  // this layer's arrival counter
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
     g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
@@ -646,50 +625,27 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.no_merge = b1_merge ? 1 : 0;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
     at.out = x->att;
-    bool fused = false;
-    if (fuse) {  // attention + merging o-proj as one launch (launch_attn_oproj)
-      AttnArgs fa = at;
-      fa.no_merge = 2;
-      fa.fuse_nsplit = rs.nsplit;
-      fa.fuse_counter = x->fuse_cnt + (size_t)li * 32;
-      fa.fuse_status = x->fuse_status_dev;
-      GemvArgs fo{};
-      attach_ws(x, fo);
-      fo.R = 1; fo.W = l.wo; fo.wscale = l.so; fo.wdtype = c.wdtype; fo.N = H; fo.K = QD;
-      fo.X = x->att; fo.xstride = QD; fo.Y = rs.h; fo.ystride = H;
-      fo.att_ml = x->part_ml; fo.att_acc = x->part_acc; fo.att_S = 32 * rs.nw * rs.cpw;
-      fo.att_stride = at.split_stride; fo.att_nsm = rs.nsplit; fo.heads = c.heads;
-      fo.kv_heads = c.kv_heads; fo.row_pos = rs.pos;
-      PROF_BEGIN(PK_ATTN);
-      e = launch_attn_oproj(fa, fo, rs.max_len, x->att_fuse, st);
-      PROF_END();
-      if (e != hipErrorNotSupported && e != hipSuccess) break;
-      fused = e == hipSuccess;
-      e = hipSuccess;
+    PROF_BEGIN(PK_ATTN);
+    e = launch_attention(at, rs.R, rs.max_len, st);
+    PROF_END();
+    if (e != hipSuccess) break;
+    // O projection + residual
+    GemvArgs o{};
+    attach_ws(x, o);
+    o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
+    o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
+    if (x->rows_frag) o.Wf = l.wo_f;
+    if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
+      if (o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step faster
+                                  // than 1 row per wave (fewer partial re-reads)
+      o.att_ml = x->part_ml; o.att_acc = x->part_acc; o.att_S = 32 * rs.nw * rs.cpw;
+      o.att_stride = at.split_stride; o.att_nsm = rs.nsplit; o.heads = c.heads;
+      o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
     }
-    if (!fused) {
-      PROF_BEGIN(PK_ATTN);
-      e = launch_attention(at, rs.R, rs.max_len, st);
-      PROF_END();
-      if (e != hipSuccess) break;
-      // O projection + residual
-      GemvArgs o{};
-      attach_ws(x, o);
-      o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
-      o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
-      if (x->rows_frag) o.Wf = l.wo_f;
-      if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
-        if (o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step faster
-                                    // than 1 row per wave (fewer partial re-reads)
-        o.att_ml = x->part_ml; o.att_acc = x->part_acc; o.att_S = 32 * rs.nw * rs.cpw;
-        o.att_stride = at.split_stride; o.att_nsm = rs.nsplit; o.heads = c.heads;
-        o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
-      }
-      PROF_BEGIN(PK_O);
-      e = launch_gemv(o, EPI_RESID, false, st);
-      PROF_END();
-      if (e != hipSuccess) break;
-    }  // !fused
+    PROF_BEGIN(PK_O);
+    e = launch_gemv(o, EPI_RESID, false, st);
+    PROF_END();
+    if (e != hipSuccess) break;
     // gate/up + SiLU*up
     GemvArgs gu{};
     attach_ws(x, gu);
@@ -844,8 +800,6 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (x->att_fuse && x->fuse_status_host && *reinterpret_cast<volatile int*>(x->fuse_status_host))
-    MX_FAIL(x, MX_ERR_HIP, "a fused attention / o-proj launch gave up waiting: results invalid");
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid
   const int ml = decode_max_len(x, n_rows);
@@ -1039,18 +993,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
-  } else if (k == "rows_gen") {
-    if (value != 4 && value != 5) MX_FAIL(x, MX_ERR_ARG, "rows_gen must be 4 or 5");
-    x->rows_gen = value;
-  } else if (k == "att_fuse") {
-    if (value < 0 || value > 4) MX_FAIL(x, MX_ERR_ARG, "att_fuse must be 0..4");
-    x->att_fuse = value;
-  } else if (k == "head_gemv1") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_gemv1 must be 0 or 1");
-    x->head_gemv1 = value;
-  } else if (k == "rows5_wpb") {
-    if (value != 0 && value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "rows5_wpb must be 0, 4 or 8");
-    x->rows5_wpb = value;
   } else if (k == "rows_frag") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
     x->rows_frag = value;
@@ -1167,7 +1109,6 @@ extern "C" void mx_llm_destroy(mx_llm* x) {
   if (x->cap) (void)hipStreamDestroy(x->cap);
   for (void* p : x->allocs) (void)hipFree(p);
   if (x->hist_host) (void)hipHostFree(x->hist_host);
-  if (x->fuse_status_host) (void)hipHostFree(x->fuse_status_host);
   delete x;
 }
 

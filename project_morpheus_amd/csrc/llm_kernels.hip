@@ -14,15 +14,6 @@
 
 namespace mx {
 
-// Write-through (agent-scope relaxed atomic = sc1) store / load of one float: the forms of the
-// in-launch hand-offs (MI355X_MICROARCH.md "Valid forms", row 1).
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // ---------------------------------------------------------------------------------
 // Weight-streaming GEMV with fused prologue (RMSNorm) and epilogues.
 //   y[r][n] = sum_k W[n][k] * xn[r][k]   for r in the block's RT activation rows.
@@ -266,26 +257,7 @@ struct MergeIn {  // one 8-dim group's split partials, loaded
   float2 ml[NSM];
   float4 lo[NSM], hi[NSM];
 };
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-// sc1 (write-through) 8- / 16-byte loads of a handed-off buffer, element offset in floats
-__device__ __forceinline__ float2 ld2_sc1(const float* base, size_t idx) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
-  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(idx * 4), 0, 16);
-  return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-}
-__device__ __forceinline__ float4 ld4_sc1(const float* base, size_t idx) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                     __uint_as_float(v.w));
-}
-
-// SC1: the partials were written in the same launch (fused attention + o-proj): every load of
-// them is an sc1 load (MI355X_MICROARCH.md "Valid forms", row 1)
-template <int NSM, bool SC1 = false>
+template <int NSM>
 __device__ __forceinline__ void merge_load(const GemvArgs& a, int j, int ns, MergeIn<NSM>& in) {
   const int GRP = a.heads / a.kv_heads;
   const int hh = j >> 4, d0 = (j & 15) * 8;
@@ -294,16 +266,10 @@ __device__ __forceinline__ void merge_load(const GemvArgs& a, int j, int ns, Mer
 #pragma unroll
   for (int s = 0; s < NSM; ++s) {
     const size_t sp = pb + min(s, ns - 1);
-    if constexpr (SC1) {
-      in.ml[s] = ld2_sc1(a.att_ml, (sp * GRP + hin) * 2);
-      in.lo[s] = ld4_sc1(a.att_acc, (sp * GRP + hin) * 128 + d0);
-      in.hi[s] = ld4_sc1(a.att_acc, (sp * GRP + hin) * 128 + d0 + 4);
-    } else {
-      in.ml[s] = *reinterpret_cast<const float2*>(a.att_ml + (sp * GRP + hin) * 2);
-      const float4* ac = reinterpret_cast<const float4*>(a.att_acc + (sp * GRP + hin) * 128 + d0);
-      in.lo[s] = ac[0];
-      in.hi[s] = ac[1];
-    }
+    in.ml[s] = *reinterpret_cast<const float2*>(a.att_ml + (sp * GRP + hin) * 2);
+    const float4* ac = reinterpret_cast<const float4*>(a.att_acc + (sp * GRP + hin) * 128 + d0);
+    in.lo[s] = ac[0];
+    in.hi[s] = ac[1];
   }
 }
 template <int NSM>
@@ -328,21 +294,8 @@ __device__ __forceinline__ void merge_apply(const MergeIn<NSM>& in, int ns, floa
   for (int i = 0; i < 8; ++i) x[i] = num[i] * inv;
 }
 
-// FUSE (the R = 1 o-projection launched together with the attention blocks it merges,
-// attn_oproj_kernel): the block's weight loads go out first, then wave 0 polls the attention
-// blocks' arrival counter (sc1 loads, bounded: a give-up sets *status and the launch runs
-// through with invalid results; the host refuses the next step), the block meets at a barrier
-// and every partial is read with sc1 loads.
-struct FuseWait {
-  const int* counter;
-  int target;
-  int* status;
-};
-// ACQ (with FUSE): after the poll one agent-scope acquire (L2 / L1 invalidate) and plain,
-// cacheable partial loads -- the guide's "Consumer, always" form -- instead of sc1 loads
-template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8, int NSM = 0, bool FUSE = false,
-          bool ACQ = false>
-__device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, const FuseWait fw) {
+template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8, int NSM = 0>
+__global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
   constexpr int NT = WPB * 64;
   constexpr int EPC = F8 ? 16 : 8;             // weights per 16-byte chunk
   constexpr int PL = EPC / 4;                  // float4 planes of the staged activation
@@ -351,9 +304,8 @@ __device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, co
   __shared__ __attribute__((aligned(16))) float4 xs[PL * KC];  // plane q at [q * KC + m]
   __shared__ float red[WPB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (a.zero_word && bid == 0 && tid == 0) *a.zero_word = 0;
   const int G = a.N / RPW;
-  int g = bid * WPB + wid;
+  int g = blockIdx.x * WPB + wid;
   const bool active = g < G;
   g = active ? g : G - 1;
   const int n0 = g * RPW;
@@ -368,7 +320,7 @@ __device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, co
   if constexpr (NSM > 0) {
     const int L = a.row_pos[0] + 1;
     ns = (L + a.att_S - 1) / a.att_S;
-    if constexpr (!FUSE) merge_load<NSM>(a, min(tid, NG - 1), ns, mi);  // partials go first
+    merge_load<NSM>(a, min(tid, NG - 1), ns, mi);  // group tid's partial loads go first
   } else {
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
@@ -399,29 +351,10 @@ __device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, co
   __builtin_amdgcn_sched_barrier(0);
 
   // 3. prologue under the weight latency
-  if constexpr (FUSE) {  // the attention partials of this launch
-    if (wid == 0) {
-      for (int it = 0;; ++it) {
-        const int v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(const_cast<int*>(fw.counter), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (v >= fw.target) break;
-        if (it > (1 << 22)) {  // ~0.3 s: the grid cannot make progress; fail loudly
-          if (lane == 0) __hip_atomic_store(fw.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if constexpr (ACQ) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-  }
   if constexpr (NSM > 0) {
     // merged 8-dim group j -> chunk m = 8j / EPC, planes q0, q0 + 1 of the staged layout
     for (int j = tid; j < NG; j += NT) {
-      if (FUSE || j != tid) merge_load<NSM, FUSE && !ACQ>(a, j, ns, mi);
+      if (j != tid) merge_load<NSM>(a, j, ns, mi);
       float xm[8];
       merge_apply<NSM>(mi, ns, xm);
       const int m = (8 * j) / EPC, q0 = ((8 * j) % EPC) / 4;
@@ -499,35 +432,6 @@ __device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, co
     acc[r] = wave_sum(acc[r]);
     if (F8) acc[r] *= wsc[r];
   }
-  if constexpr (EPI == EPI_ARGMAX) {
-    // lm_head: penalty on the slot's seen set, logits kept for sampling / parity reads, the
-    // block's best (value, smallest index) key merged into best[0] with one atomicMax
-    __shared__ unsigned long long bkey[WPB];
-    unsigned long long key = 0ull;
-    if (active) {
-      const int slot = a.row_slot[0];
-      const uint8_t* seen = a.seen + (size_t)slot * a.N;
-      const float pen = a.penalty[slot];
-      const bool keep = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) {
-        float v = acc[r];
-        if (seen[n0 + r]) v = v > 0.f ? v / pen : v * pen;
-        if (keep && lane == r) a.logits[n0 + r] = v;
-        const unsigned long long k = argmax_key(v, (uint32_t)(n0 + r));
-        key = k > key ? k : key;
-      }
-    }
-    if (lane == 0) bkey[wid] = key;
-    __syncthreads();
-    if (tid == 0) {
-      unsigned long long k = bkey[0];
-#pragma unroll
-      for (int i = 1; i < WPB; ++i) k = bkey[i] > k ? bkey[i] : k;
-      if (k) atomicMax(a.best, k);
-    }
-    return;
-  }
   if (!active || lane != 0) return;
 
   // 5. epilogues
@@ -574,11 +478,6 @@ __device__ __forceinline__ void gemv1_block(const GemvArgs& a, const int bid, co
   }
 }
 
-template <int KCH, int RPW, int EPI, bool NORM, int WPB, bool F8, int NSM = 0>
-__global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
-  gemv1_block<KCH, RPW, EPI, NORM, WPB, F8, NSM>(a, blockIdx.x, FuseWait{nullptr, 0, nullptr});
-}
-
 // ---------------------------------------------------------------------------------
 // Decode / prefill attention on bf16 MFMA, one launch: split-KV partials + in-launch merge.
 //   Grid (nsplit, kv_heads, R), block 256 = 4 waves; a wave owns CPW chunks of 32 positions
@@ -600,6 +499,12 @@ __global__ __launch_bounds__(WPB * 64) void gemv1_kernel(GemvArgs a) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // x = p0 + p1 + p2 with p_i bf16 (exact to fp32 rounding); 8 values -> three fragments
 __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, bf16x8& f2) {
   uint32_t w0[4], w1[4], w2[4];
@@ -621,11 +526,11 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
 // flight under the current chunk's MFMAs and softmax.  NW = 8, CPW = 4 covers
 // 1,024 positions in one block, so a single-row step up to that length needs no split merge.
 template <int GRP, int CPW, int NW>
-__device__ __forceinline__ void attn_block(const AttnArgs& a, const int split, const int kvh,
-                                           const int r) {
+__global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
   constexpr int S = 32 * NW * CPW;
   constexpr int NT = NW * 64;
   constexpr int KM = (GRP * 128 + NT - 1) / NT;  // (head, dim) outputs per thread in merges
+  const int split = blockIdx.x, kvh = blockIdx.y, r = blockIdx.z;
   const int L = a.row_pos[r] + 1;
   const int nsplit = (L + S - 1) / S;
   if (split >= nsplit) return;
@@ -807,18 +712,10 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int split, c
       const int idx = tid + NT * k;
       if (idx < GRP * 128) {
         const int h = idx >> 7, td = idx & 127;
-        if (a.no_merge == 2) {  // same launch as the consumer: write-through (sc1) stores
-          st_wt(a.part_acc + (pb * GRP + h) * 128 + td, bn[k]);
-          if (td == 0) {
-            st_wt(a.part_ml + (pb * GRP + h) * 2, bm[k]);
-            st_wt(a.part_ml + (pb * GRP + h) * 2 + 1, bl[k]);
-          }
-        } else {
-          a.part_acc[(pb * GRP + h) * 128 + td] = bn[k];
-          if (td == 0) {
-            a.part_ml[(pb * GRP + h) * 2] = bm[k];
-            a.part_ml[(pb * GRP + h) * 2 + 1] = bl[k];
-          }
+        a.part_acc[(pb * GRP + h) * 128 + td] = bn[k];
+        if (td == 0) {
+          a.part_ml[(pb * GRP + h) * 2] = bm[k];
+          a.part_ml[(pb * GRP + h) * 2 + 1] = bl[k];
         }
       }
     }
@@ -894,67 +791,6 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int split, c
     }
     out[idx] = num / den;
   }
-}
-
-template <int GRP, int CPW, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
-  attn_block<GRP, CPW, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z);
-}
-
-// One-row step: attention + o-projection in ONE launch.  Blocks [0, nsplit * kv_heads) are the
-// attention splits (4 waves, partials written through, then one arrival on the counter --
-// blocks past the row's context arrive too); the rest are the o-projection GEMV blocks, which
-// stream their weights at once and only then wait for the attention blocks.  Attention is
-// latency-bound and leaves HBM idle for most of its ~6 us: the o-projection's 18.9 MB (bf16)
-// stream in that time instead of after it.  Every block an o-proj block waits on has a smaller
-// index, so it was dispatched first and is resident or done: the grid cannot deadlock.
-// NW waves per block for both roles: the o-projection blocks hold 16 rows (16 / NW per wave).
-template <int GRP, int CPW, int NW, int KCH, bool F8, int NSM, bool ACQ>
-__global__ __launch_bounds__(NW * 64) void attn_oproj_kernel(AttnArgs at, GemvArgs o) {
-  const int nA = at.fuse_nsplit * at.kv_heads;
-  if ((int)blockIdx.x < nA) {
-    attn_block<GRP, CPW, NW>(at, blockIdx.x % at.fuse_nsplit, blockIdx.x / at.fuse_nsplit, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(at.fuse_counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  gemv1_block<KCH, 16 / NW, EPI_RESID, false, NW, F8, NSM, true, ACQ>(
-      o, blockIdx.x - nA, FuseWait{at.fuse_counter, nA, at.fuse_status});
-}
-
-// mode (option att_fuse): 1 = 4-wave blocks, sc1 partial loads; 2 = 4-wave, acquire + plain
-// loads; 3 / 4 = the same with 8-wave blocks (attention 8 x 32 positions per split)
-hipError_t launch_attn_oproj(const AttnArgs& at, const GemvArgs& o, int max_len, int mode,
-                             hipStream_t st) {
-  const bool f8 = o.wdtype == WT_FP8;
-  const int grp = at.heads / at.kv_heads;
-  const int nw = mode >= 3 ? 8 : 4;
-  const bool acq = mode == 2 || mode == 4;
-  if (at.nw != nw || o.K % (f8 ? 1024 : 512) || o.N % 16 || !at.fuse_counter)
-    return hipErrorNotSupported;
-  const int kch = o.K / (f8 ? 1024 : 512);
-  const int S = 32 * nw * at.cpw;
-  const int nsplit = (max_len + S - 1) / S;
-  if (nsplit > 8 || nsplit != at.fuse_nsplit) return hipErrorNotSupported;
-  const int nsm = nsplit <= 4 ? 4 : 8;
-  const dim3 grid(nsplit * at.kv_heads + o.N / 16), blk(64 * nw);
-#define MX_AO(G_, C_, W_, K_, F_, M_, A_)                                                      \
-  if (grp == G_ && at.cpw == C_ && nw == W_ && kch == K_ && f8 == F_ && nsm == M_ && acq == A_) { \
-    hipLaunchKernelGGL((attn_oproj_kernel<G_, C_, W_, K_, F_, M_, A_>), grid, blk, 0, st, at, o); \
-    return hipGetLastError();                                                                  \
-  }
-#define MX_AOM(G_, C_, W_, K_, F_) MX_AO(G_, C_, W_, K_, F_, 4, false) MX_AO(G_, C_, W_, K_, F_, 8, false) \
-                                   MX_AO(G_, C_, W_, K_, F_, 4, true) MX_AO(G_, C_, W_, K_, F_, 8, true)
-#define MX_AOG(G_, K_, F_) MX_AOM(G_, 1, 4, K_, F_) MX_AOM(G_, 2, 4, K_, F_) \
-                           MX_AOM(G_, 1, 8, K_, F_) MX_AOM(G_, 2, 8, K_, F_)
-  MX_AOG(3, 6, false) MX_AOG(3, 3, true)   // Orpheus widths
-  MX_AOG(2, 1, false) MX_AOG(4, 1, true)   // the small test configurations
-#undef MX_AOG
-#undef MX_AOM
-#undef MX_AO
-  return hipErrorNotSupported;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1134,8 +970,7 @@ static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_
   MX_G1(KCH_, 2, EPI_QKV, true) MX_G1(KCH_, 1, EPI_RESID, false)                       \
   MX_G1(KCH_, 2, EPI_RESID, false)                                                      \
   MX_G1(KCH_, 2, EPI_SILU, true) MX_G1(KCH_, 4, EPI_SILU, true)                         \
-  MX_G1(KCH_, 1, EPI_STORE, false) MX_G1(KCH_, 1, EPI_STORE, true)                     \
-  MX_G1(KCH_, 4, EPI_ARGMAX, true)
+  MX_G1(KCH_, 1, EPI_STORE, false) MX_G1(KCH_, 1, EPI_STORE, true)
   MX_G1K(1) MX_G1K(2) MX_G1K(3) MX_G1K(4) MX_G1K(6) MX_G1K(8) MX_G1K(16)
 #undef MX_G1K
 #undef MX_G1
@@ -1143,12 +978,6 @@ static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_
 }
 
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
-  if (a.R == 1 && epi == EPI_ARGMAX && a.head_gemv1 && !a.force_legacy) {
-    GemvArgs h = a;
-    h.rpw = 4;
-    const hipError_t e = launch_gemv1(h, epi, norm, st);
-    if (e != hipErrorNotSupported) return e;
-  }
   if (a.R == 1 && epi != EPI_ARGMAX && !a.force_legacy) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.att_ml) return e;  // (the merge has no other kernel)
@@ -1160,12 +989,7 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const int blocks = gemv_blocks(a.N, 8, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
     return launch_gemv_t<1, 8, EPI_ARGMAX, true, true>(a, blocks, st);
   }
-  // multi-row steps (and any other fp8 shape) run on the MFMA kernels: generation 5 for
-  // decode rows (<= 64), generation 4 for prefill rows and any shape generation 5 skips
-  if (a.rows_gen == 5 && a.R >= 2 && !a.force_legacy) {
-    const hipError_t e = v5::launch_gemm_rows_v5(a, epi, norm, st);
-    if (e != hipErrorNotSupported) return e;
-  }
+  // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
     const hipError_t e = v4::launch_gemm_rows_v4(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.wdtype == WT_FP8) return e;

@@ -40,10 +40,6 @@ struct GemvArgs {
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
-  int rows_gen;            // multi-row decode GEMM generation for R <= 64: 5 (full-K tiles), 4
-  int rows5_wpb;           // generation 5: waves per block (0 = per-epilogue default)
-  int head_gemv1;          // R = 1 lm_head on the load-first gemv1 kernel (4 rows per wave)
-  int* zero_word;          // R = 1 GEMV: block 0 zeroes this word first (a fused-launch counter)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -83,12 +79,7 @@ struct AttnArgs {
   int* counter;            // [R][kv_heads] split arrival tickets (zero between launches)
   float* out;              // [R][heads*128]
   int debug;               // timing experiments only (0 in the product path)
-  int no_merge;            // 1: every split stores its partial, the consumer merges (R = 1);
-                           // 2: the same with write-through stores (fused launch)
-  // R = 1 fused attention + o-projection launch (launch_attn_oproj)
-  int fuse_nsplit;         // attention splits of the launch grid
-  int* fuse_counter;       // attention blocks arrived (zeroed by the layer's qkv GEMV)
-  int* fuse_status;        // host-mapped: 1 once a wait gave up (results invalid)
+  int no_merge;            // 1: every split stores its partial, the consumer merges (R = 1)
 };
 
 struct CommitArgs {
@@ -108,9 +99,6 @@ struct CommitArgs {
 
 hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-namespace v5 {  // multi-row decode GEMM generation 5 (mx_rows_v5.inc)
-hipError_t launch_gemm_rows_v5(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-}  // namespace v5
 namespace v4 {  // multi-row GEMM generation 4 (mx_rows_v4.inc)
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
@@ -135,10 +123,6 @@ hipError_t launch_set_scalar(float* p, float v, hipStream_t st);
 hipError_t launch_move_row(int32_t* slot, int32_t* pos, int32_t* token, float* h, int hidden,
                            int dst, int src, int scratch, hipStream_t st);
 hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st);
-// R = 1: attention (no_merge = 2) and the merging o-projection (EPI_RESID, 4-wave blocks of 16
-// rows) in ONE launch; hipErrorNotSupported for shapes without an instantiation.
-hipError_t launch_attn_oproj(const AttnArgs& at, const GemvArgs& o, int max_len, int mode,
-                             hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, int R, hipStream_t st);
 hipError_t launch_embed_rows(const int32_t* ids, int n, int slot, const uint16_t* embed,
                              int hidden, int vocab, uint8_t* seen, float* h, hipStream_t st);

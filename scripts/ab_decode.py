@@ -16,8 +16,7 @@ sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
-            "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_gen": 4,
-            "rows5_wpb": 0, "head_gemv1": 0, "att_fuse": 0}
+            "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -34,15 +33,7 @@ VARIANTS = {
     "t384": {"rows_target": 384},
     "t512": {"rows_target": 512},
     "pw1": {"rows_pw": 1},
-    "v5": {"rows_gen": 5},
-    "v5_w4": {"rows_gen": 5, "rows5_wpb": 4},
-    "v5_w8": {"rows_gen": 5, "rows5_wpb": 8},
-    "head1": {"head_gemv1": 1},
-    "fuse": {"att_fuse": 1},
-    "fuse2": {"att_fuse": 2},
     "nw8": {"att_cpw": 1, "att_nw": 8},
-    "fuse3": {"att_fuse": 3, "att_cpw": 1, "att_nw": 8},
-    "fuse4": {"att_fuse": 4, "att_cpw": 1, "att_nw": 8},
 }
 
 
