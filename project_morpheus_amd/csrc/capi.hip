@@ -134,6 +134,8 @@ struct mx_llm {
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
+  int head_kct = 0;                  // option: one-row lm_head with every load issued first
+  int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
@@ -569,6 +571,8 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_target = x->rows_target;
   g.rows_nt_max = x->rows_nt_max;
   g.rows_head_target = x->rows_head_target;
+  g.head_kct = x->head_kct;
+  g.rows_head_mt = x->rows_head_mt;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
   g.tickets = x->rows_tickets;
@@ -993,6 +997,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   const std::string k(key);
   if (k == "legacy_gemv") {
     x->legacy_gemv = value;
+  } else if (k == "rows_head_mt") {
+    if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_head_mt must be 1 or 2");
+    x->rows_head_mt = value;
+  } else if (k == "head_kct") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_kct must be 0 or 1");
+    x->head_kct = value;
   } else if (k == "rows_frag") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
     x->rows_frag = value;

@@ -40,6 +40,8 @@ struct GemvArgs {
   int rows_target;         // generation 4: blocks the K-range split aims for (0 = per shape)
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
+  int head_kct;            // R = 1 lm_head: K known at compile time, all loads first (K = 3072)
+  int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;

@@ -11,6 +11,12 @@ hipError_t launch_rows_head(const GemvArgs& a, int epi, bool norm, int nt, hipSt
     if (nt == 2) return launch_rows_k<1, 2, EPI_, NORM_>(a, st);                          \
     return launch_rows_k<1, 4, EPI_, NORM_>(a, st);                                       \
   }
+  // option rows_head_mt = 2: 32 weight rows per wave (256 per block), so every staged
+  // activation sub-chunk feeds twice the lm_head weights (half the activation re-reads)
+  if (epi == EPI_ARGMAX && norm && a.rows_head_mt == 2) {
+    if (nt == 1) return launch_rows_k<2, 1, EPI_ARGMAX, true>(a, st);
+    if (nt == 2) return launch_rows_k<2, 2, EPI_ARGMAX, true>(a, st);
+  }
   MX_R(EPI_ARGMAX, true)
   MX_R(EPI_STORE, false)
   MX_R(EPI_STORE, true)

@@ -23,4 +23,5 @@ fi
 [ -z "${AB1:-}" ] || step ab1 400 python -u scripts/ab_decode.py $AB1
 [ -z "${AB2:-}" ] || step ab2 400 python -u scripts/ab_decode.py $AB2
 [ -z "${AB3:-}" ] || step ab3 400 python -u scripts/ab_decode.py $AB3
+[ -z "${AB4:-}" ] || step ab4 400 python -u scripts/ab_decode.py $AB4
 exit 0
