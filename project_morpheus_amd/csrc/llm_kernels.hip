@@ -1031,6 +1031,11 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const int blocks = gemv_blocks(a.N, 4, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
     return launch_gemv_t<1, 4, EPI_ARGMAX, true, false, 6>(a, blocks, st);
   }
+  // a few rows (option small_rows): the VALU small-batch GEMV
+  if (a.R >= 2 && a.R <= a.small_rows && !a.force_legacy) {
+    const hipError_t e = launch_gemv_small(a, epi, norm, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
     const hipError_t e = v4::launch_gemm_rows_v4(a, epi, norm, st);
@@ -1084,6 +1089,7 @@ hipError_t gemv_prepare(int kmax) {
   if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 4, EPI_ARGMAX, true, false, 6>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
+  if (e == hipSuccess) e = gemv_small_prepare();
   return e;
 }
 

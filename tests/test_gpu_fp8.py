@@ -106,6 +106,17 @@ def test_fp8_batched_orpheus_width_8_rows():
     assert _check(cfg, qw, prompts, 6) >= 0.8 * 8 * 6
 
 
+@pytest.mark.parametrize("n", [3, 8])
+def test_fp8_small_rows_valu_gemv_orpheus_width(n):
+    """configs[4]'s 8 fp8 streams on the VALU small-batch GEMV (option small_rows): e4m3
+    weights converted in registers (v_cvt_pk_f32_fp8), per-row scales, packed fp32 FMAs."""
+    cfg = C.OrpheusConfig(layers=2)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=57 + n), cfg)
+    rng = np.random.default_rng(18 + n)
+    prompts = [[int(x) for x in rng.integers(1000, 128000, 5 + 4 * i)] for i in range(n)]
+    assert _check(cfg, qw, prompts, 6, options={"small_rows": 8}) >= 0.8 * n * 6
+
+
 def test_fp8_single_stream_long_context():
     """The default fp8 one-row path over configs[1]'s context range (L 200 -> 1,260): the fp8
     merging o-proj at NSM 2 / 4 / 8 and the 256-position attention past 1,024."""

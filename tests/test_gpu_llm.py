@@ -322,6 +322,17 @@ def test_batched_decode_orpheus_width_64_rows():
     assert _compare_rows(cfg, w, _orpheus_prompts(64, 26, 3, 1), 3) >= 0.8 * 64 * 3
 
 
+@pytest.mark.parametrize("n", [2, 5, 8])
+def test_small_rows_valu_gemv_orpheus_width(n):
+    """2 <= R <= 8 rows on the VALU small-batch GEMV (rows_small.hip, option small_rows):
+    one row tile at 2 (RT 4), two tiles of the K = ffn down projection at 5 and 8, the
+    lm_head's penalty/argmax epilogue over 78,470 row pairs, ragged prompts."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=60 + n)
+    assert _compare_rows(cfg, w, _orpheus_prompts(n, 61 + n, 4, 3), 6,
+                         options={"small_rows": 8}) >= 0.8 * n * 6
+
+
 @pytest.mark.parametrize("head_target", [2048, 4096])
 def test_batched_lm_head_k_split_orpheus_width(head_target):
     """The multi-row lm_head split over 2 / 4 K ranges (option rows_head_target): the last
