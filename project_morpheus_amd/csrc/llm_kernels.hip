@@ -20,9 +20,7 @@ namespace mx {
 // Grid: x = row-group workers (grid-stride over N / RPW groups, one wave per group),
 //       y = ceil(R / RT) activation-row tiles.
 // ---------------------------------------------------------------------------------
-// KCT > 0: K is known (KCT 16-byte chunks per lane per row, KCT * 64 chunks per row): the
-// whole row group's weight loads are issued before any FMA (the lm_head: 24 loads per lane)
-template <int RT, int RPW, int EPI, bool NORM, bool F8 = false, int KCT = 0>
+template <int RT, int RPW, int EPI, bool NORM, bool F8 = false>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K8 = a.K >> 3;
@@ -99,42 +97,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
       wp[i] = F8 ? reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(a.W) + (size_t)n * a.K)
                  : reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.W) + (size_t)n * a.K);
     }
-    if constexpr (KCT > 0) {  // every load of the row group first, then the FMAs
-      uint4 w[RPW][KCT];
-#pragma unroll
-      for (int j = 0; j < KCT; ++j)
-#pragma unroll
-        for (int i = 0; i < RPW; ++i) w[i][j] = load_nt(wp[i] + j * 64 + lane);
-#pragma unroll
-      for (int j = 0; j < KCT; ++j) {
-        const int c = j * 64 + lane;
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          if (F8) {
-            const float4 x0 = xlo[rt * K8 + 2 * c], x1 = xhi[rt * K8 + 2 * c];
-            const float4 x2 = xlo[rt * K8 + 2 * c + 1], x3 = xhi[rt * K8 + 2 * c + 1];
-#pragma unroll
-            for (int i = 0; i < RPW; ++i) {
-              const uint32_t wd[4] = {w[i][j].x, w[i][j].y, w[i][j].z, w[i][j].w};
-              const float4 xx[4] = {x0, x1, x2, x3};
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
-                const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
-                acc[i][rt] = fmaf(lo.x, xx[q].x, acc[i][rt]);
-                acc[i][rt] = fmaf(lo.y, xx[q].y, acc[i][rt]);
-                acc[i][rt] = fmaf(hi.x, xx[q].z, acc[i][rt]);
-                acc[i][rt] = fmaf(hi.y, xx[q].w, acc[i][rt]);
-              }
-            }
-          } else {
-            const float4 lo = xlo[rt * K8 + c], hi = xhi[rt * K8 + c];
-#pragma unroll
-            for (int i = 0; i < RPW; ++i) acc[i][rt] = dot8(w[i][j], lo, hi, acc[i][rt]);
-          }
-        }
-      }
-    } else if (F8) {  // 16 e4m3 weights per 16-byte chunk = activation chunks 2c, 2c+1
+    if (F8) {  // 16 e4m3 weights per 16-byte chunk = activation chunks 2c, 2c+1
 #pragma unroll 4
       for (int c = lane; c < (K8 >> 1); c += 64) {
         uint4 w[RPW];
@@ -950,12 +913,12 @@ __global__ void to_f32_kernel(float* dst, const void* src, int64_t n, int src_bf
 // ---------------------------------------------------------------------------------
 // Host-side launchers
 // ---------------------------------------------------------------------------------
-template <int RT, int RPW, int EPI, bool NORM, bool F8 = false, int KCT = 0>
+template <int RT, int RPW, int EPI, bool NORM, bool F8 = false>
 static hipError_t launch_gemv_t(const GemvArgs& a, int blocks, hipStream_t st) {
   const size_t lds = (size_t)RT * a.K * 4 + 64;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int ytiles = (a.R + RT - 1) / RT;
-  hipLaunchKernelGGL((gemv_kernel<RT, RPW, EPI, NORM, F8, KCT>), dim3(blocks, ytiles), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemv_kernel<RT, RPW, EPI, NORM, F8>), dim3(blocks, ytiles), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
@@ -1019,17 +982,16 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.att_ml) return e;  // (the merge has no other kernel)
   }
+  if (a.R == 1 && epi == EPI_ARGMAX && a.small_head && !a.force_legacy) {
+    const hipError_t e = launch_gemv_small(a, epi, norm, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   // fp8 single-row lm_head: the grid-stride argmax GEMV with e4m3 weights
   // (8 rows per wave: an e4m3 row is 3 KB, so 4 rows left a wave only 12 loads of 16 B in
   // flight; measured 106.8 us = 4.5 TB/s at 4 rows)
   if (a.R == 1 && epi == EPI_ARGMAX && norm && a.wdtype == WT_FP8 && a.K % 1024 == 0) {
     const int blocks = gemv_blocks(a.N, 8, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
-    if (a.head_kct && a.K == 3072) return launch_gemv_t<1, 8, EPI_ARGMAX, true, true, 3>(a, blocks, st);
     return launch_gemv_t<1, 8, EPI_ARGMAX, true, true>(a, blocks, st);
-  }
-  if (a.R == 1 && epi == EPI_ARGMAX && norm && a.head_kct && a.K == 3072 && !a.force_legacy) {
-    const int blocks = gemv_blocks(a.N, 4, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
-    return launch_gemv_t<1, 4, EPI_ARGMAX, true, false, 6>(a, blocks, st);
   }
   // a few rows (option small_rows): the VALU small-batch GEMV
   if (a.R >= 2 && a.R <= a.small_rows && !a.force_legacy) {
@@ -1082,12 +1044,6 @@ hipError_t gemv_prepare(int kmax) {
 #undef MX_A
   if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 8, EPI_ARGMAX, true, true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
-  if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 8, EPI_ARGMAX, true, true, 3>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
-  if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 4, EPI_ARGMAX, true, false, 6>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
   if (e == hipSuccess) e = gemv_small_prepare();
   return e;

@@ -1,4 +1,5 @@
-// Small-batch decode GEMV (2 <= R <= 8 activation rows) on the VALU, for MI355X (gfx950).
+// Small-batch decode GEMV (2 <= R <= 8 activation rows; R = 1 for the lm_head) on the VALU,
+// for MI355X (gfx950).
 //
 // The B = 1 kernel (gemv1_kernel) streams every weight row once with all of a wave's loads
 // issued first; this is the same design for a handful of rows.  Each wave owns RPW whole
@@ -42,13 +43,53 @@ __device__ __forceinline__ void load_group(const GemvArgs& a, int g, int lane, u
     for (int c = 0; c < KCH; ++c) w[r][c] = load_nt(wp + (size_t)r * KC + c * 64);
 }
 
+template <int EPI>
+constexpr int pair_of() { return (EPI == EPI_SILU || EPI == EPI_QKV) ? 2 : 1; }
+
+// Lane j < NOUT = RPW / PAIR x RT owns output j of every group: weight row (pair) ri,
+// activation row t of the tile; its row constants are loaded once.
+struct LaneOut {
+  int ri, t, r;  // r: the activation row (clamped into the tile for idle lanes)
+  bool on;
+  int slot, pos;
+  float pen;
+  bool keep;
+};
+
+// Epilogue operands of one group, loaded BEFORE the next group's weight loads: the load
+// counter is in order, so a load issued after them would make the epilogue wait for the
+// whole prefetch.  Every address is valid (clamped), so no load is predicated.
+struct EpiIn {
+  float y, ws0, ws1, cs, sn;
+  uint8_t seen;
+};
+
+template <int RPW, int EPI, bool F8>
+__device__ __forceinline__ EpiIn epi_load(const GemvArgs& a, int g, const LaneOut& L) {
+  EpiIn e{};
+  const int n = g * RPW + L.ri;
+  if (EPI == EPI_RESID) e.y = a.Y[(size_t)L.r * a.ystride + n];
+  if (F8) {
+    e.ws0 = a.wscale[n];
+    if (pair_of<EPI>() == 2) e.ws1 = a.wscale[n + 1];
+  }
+  if (EPI == EPI_QKV) {
+    const int p = (n & 127) >> 1;
+    e.cs = a.rope_cos[(size_t)L.pos * 64 + p];
+    e.sn = a.rope_sin[(size_t)L.pos * 64 + p];
+  }
+  if (EPI == EPI_ARGMAX) e.seen = a.seen[(size_t)L.slot * a.N + n];
+  return e;
+}
+
 template <int KCH, int RPW, int RT, int EPI, bool F8>
-__device__ __forceinline__ void process(const GemvArgs& a, const float4* xs, int g, int r0,
-                                        int nr, int lane, const uint4 (&w)[RPW][KCH],
-                                        unsigned long long& best) {
+__device__ __forceinline__ void process(const GemvArgs& a, const float4* xs, int g, int lane,
+                                        const uint4 (&w)[RPW][KCH], const LaneOut& L,
+                                        const EpiIn& e, unsigned long long& best) {
   constexpr int EPC = F8 ? 16 : 8;
   constexpr int PL = EPC / 4;
   constexpr int KC = KCH * 64;
+  constexpr int PAIR = pair_of<EPI>();
   // the staged rows are loop-invariant: an opaque copy of the lane index keeps the compiler
   // from hoisting every group's LDS reads (RT x KCH x PL float4) out of the group loop
   int xl = lane;
@@ -88,73 +129,71 @@ __device__ __forceinline__ void process(const GemvArgs& a, const float4* xs, int
       }
     }
   }
-  float s[RPW][RT];
+  // transposing butterfly: each exchange halves the values a lane carries, so RPW x RT
+  // totals cost NV - 1 + log2(64 / NV) shuffles instead of 6 NV; afterwards the 64 / NV
+  // consecutive lanes from SPAN * f hold total f = r * RT + t
+  constexpr int NV = RPW * RT;
+  float v[NV];
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
-    for (int t = 0; t < RT; ++t) s[r][t] = wave_sum(acc[r][t].x + acc[r][t].y);
-  const int n0 = g * RPW;
-  if (F8) {
+    for (int t = 0; t < RT; ++t) v[r * RT + t] = acc[r][t].x + acc[r][t].y;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      const float sc = a.wscale[n0 + r];
+  for (int m = 32, cnt = NV; m >= 1; m >>= 1) {
+    if (cnt > 1) {
+      const bool up = lane & m;
+      cnt >>= 1;
 #pragma unroll
-      for (int t = 0; t < RT; ++t) s[r][t] *= sc;
+      for (int i = 0; i < NV / 2; ++i) {
+        if (i < cnt) {
+          const float send = up ? v[i] : v[i + cnt];
+          const float keep = up ? v[i + cnt] : v[i];
+          v[i] = keep + __shfl_xor(send, m, MX_WAVE);
+        }
+      }
+    } else {
+      v[0] += __shfl_xor(v[0], m, MX_WAVE);
     }
   }
-
-  // every lane holds every total; lane j writes output j (pairs for SILU / QKV)
-  constexpr int PAIR = (EPI == EPI_SILU || EPI == EPI_QKV) ? 2 : 1;
-  constexpr int NOUT = RPW / PAIR * RT;
-  static_assert(NOUT <= 64, "outputs per group exceed a wave");
-  float v0 = 0.f, v1 = 0.f;
-  int ri = 0, t = 0;
-#pragma unroll
-  for (int i = 0; i < RPW / PAIR; ++i)
-#pragma unroll
-    for (int tt = 0; tt < RT; ++tt)
-      if (lane == i * RT + tt) {
-        v0 = s[i * PAIR][tt];
-        if (PAIR == 2) v1 = s[i * PAIR + 1][tt];
-        ri = i * PAIR;
-        t = tt;
-      }
-  if (lane >= NOUT || t >= nr) return;
-  const int r = r0 + t, n = n0 + ri;
+  constexpr int SPAN = 64 / NV;
+  float v0 = v[0], v1 = 0.f;
+  if (PAIR == 2) v1 = __shfl(v0, (lane + RT * SPAN) & 63, MX_WAVE);  // total (r + 1, t)
+  if (F8) {
+    v0 *= e.ws0;
+    v1 *= e.ws1;
+  }
+  if (!L.on) return;
+  const int r = L.r, n = g * RPW + L.ri;
   if (EPI == EPI_RESID) {
-    a.Y[(size_t)r * a.ystride + n] += v0;
+    a.Y[(size_t)r * a.ystride + n] = e.y + v0;
   } else if (EPI == EPI_STORE) {
     a.Y[(size_t)r * a.N + n] = v0;
   } else if (EPI == EPI_SILU) {
     a.Y[(size_t)r * (a.N >> 1) + (n >> 1)] = v0 / (1.0f + expf(-v0)) * v1;
   } else if (EPI == EPI_QKV) {
-    const int slot = a.row_slot[r], pos = a.row_pos[r];
     const int hh = n >> 7, within = n & 127, p = within >> 1;
     if (hh < a.heads + a.kv_heads) {
-      const float cs = a.rope_cos[(size_t)pos * 64 + p];
-      const float sn = a.rope_sin[(size_t)pos * 64 + p];
-      const float o1 = v0 * cs - v1 * sn;
-      const float o2 = v1 * cs + v0 * sn;
+      const float o1 = v0 * e.cs - v1 * e.sn;
+      const float o2 = v1 * e.cs + v0 * e.sn;
       if (hh < a.heads) {
         float* q = a.Q + ((size_t)r * a.heads + hh) * 128;
         q[p] = o1;
         q[p + 64] = o2;
       } else {
-        uint16_t* k = a.kcache + ((size_t)slot * a.kv_heads + (hh - a.heads)) * a.max_pos * 128;
-        k[kv_k_off(pos, p)] = f32_to_bf16(o1);
-        k[kv_k_off(pos, p + 64)] = f32_to_bf16(o2);
+        uint16_t* k = a.kcache + ((size_t)L.slot * a.kv_heads + (hh - a.heads)) * a.max_pos * 128;
+        k[kv_k_off(L.pos, p)] = f32_to_bf16(o1);
+        k[kv_k_off(L.pos, p + 64)] = f32_to_bf16(o2);
       }
     } else {
       uint16_t* vc = a.vcache +
-          ((size_t)slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
-      vc[kv_v_off(pos, within)] = f32_to_bf16(v0);
-      vc[kv_v_off(pos, within + 1)] = f32_to_bf16(v1);
+          ((size_t)L.slot * a.kv_heads + (hh - a.heads - a.kv_heads)) * 128 * a.max_pos;
+      vc[kv_v_off(L.pos, within)] = f32_to_bf16(v0);
+      vc[kv_v_off(L.pos, within + 1)] = f32_to_bf16(v1);
     }
   } else if (EPI == EPI_ARGMAX) {
-    const int slot = a.row_slot[r];
     float v = v0;
-    if (a.seen[(size_t)slot * a.N + n]) v = v > 0.f ? v / a.penalty[slot] : v * a.penalty[slot];
-    if (a.logits && (a.logits_all || a.samp_temp[slot] > 0.f)) a.logits[(size_t)r * a.N + n] = v;
+    if (e.seen) v = v > 0.f ? v / L.pen : v * L.pen;
+    if (L.keep) a.logits[(size_t)r * a.N + n] = v;
     const unsigned long long key = argmax_key(v, (uint32_t)n);
     best = key > best ? key : best;
   }
@@ -183,6 +222,22 @@ __global__ __launch_bounds__(NT, 1) void gemv_small_kernel(GemvArgs a, int ytile
   const int stride = gblocks * WPB;
   int g = gb * WPB + wid;
 
+  constexpr int NV = RPW * RT;
+  static_assert(NV <= 64 && (NV & (NV - 1)) == 0, "RPW x RT must be a power of two <= 64");
+  LaneOut L{};
+  {
+    const int f = lane / (64 / NV);  // the total this lane holds after the butterfly
+    L.ri = f / RT;
+    L.t = f % RT;
+    L.on = lane % (64 / NV) == 0 && L.ri % pair_of<EPI>() == 0 && L.t < nr;
+    L.r = r0 + min(L.t, nr - 1);
+    if (EPI == EPI_QKV || EPI == EPI_ARGMAX) L.slot = a.row_slot[L.r];
+    if (EPI == EPI_QKV) L.pos = a.row_pos[L.r];
+    if (EPI == EPI_ARGMAX) {
+      L.pen = a.penalty[L.slot];
+      L.keep = a.logits && (a.logits_all || a.samp_temp[L.slot] > 0.f);
+    }
+  }
   // 1. the first group's weight loads, then the activation rows under their latency
   uint4 w0[RPW][KCH], w1[RPW][KCH];
   load_group<KCH, RPW, F8>(a, min(g, G - 1), lane, w0);
@@ -242,30 +297,35 @@ __global__ __launch_bounds__(NT, 1) void gemv_small_kernel(GemvArgs a, int ytile
   }
   __syncthreads();
 
-  // 2. the wave's groups, the next group's loads in flight under the current FMAs
+  // 2. the wave's groups, the next group's loads in flight under the current FMAs (each
+  // group's epilogue operands are loaded before that prefetch)
   unsigned long long best = 0ull;
   if (g < G) {
     while (true) {
       if (g + stride < G) {
+        const EpiIn e = epi_load<RPW, EPI, F8>(a, g, L);
         load_group<KCH, RPW, F8>(a, g + stride, lane, w1);
-        process<KCH, RPW, RT, EPI, F8>(a, xs, g, r0, nr, lane, w0, best);
+        process<KCH, RPW, RT, EPI, F8>(a, xs, g, lane, w0, L, e, best);
       } else {
-        process<KCH, RPW, RT, EPI, F8>(a, xs, g, r0, nr, lane, w0, best);
+        const EpiIn e = epi_load<RPW, EPI, F8>(a, g, L);
+        process<KCH, RPW, RT, EPI, F8>(a, xs, g, lane, w0, L, e, best);
         break;
       }
       g += stride;
       if (g + stride < G) {
+        const EpiIn e = epi_load<RPW, EPI, F8>(a, g, L);
         load_group<KCH, RPW, F8>(a, g + stride, lane, w0);
-        process<KCH, RPW, RT, EPI, F8>(a, xs, g, r0, nr, lane, w1, best);
+        process<KCH, RPW, RT, EPI, F8>(a, xs, g, lane, w1, L, e, best);
       } else {
-        process<KCH, RPW, RT, EPI, F8>(a, xs, g, r0, nr, lane, w1, best);
+        const EpiIn e = epi_load<RPW, EPI, F8>(a, g, L);
+        process<KCH, RPW, RT, EPI, F8>(a, xs, g, lane, w1, L, e, best);
         break;
       }
       g += stride;
     }
   }
-  if (EPI == EPI_ARGMAX) {  // lane i * RT + t carried row t's best over its groups
-    if (lane < RPW * RT) atomicMax(&bred[lane % RT], best);
+  if (EPI == EPI_ARGMAX) {  // an "on" lane carried its row t's best over its groups
+    if (L.on) atomicMax(&bred[L.t], best);
     __syncthreads();
     if (tid < nr) atomicMax(a.best + r0 + tid, bred[tid]);
   }
@@ -279,8 +339,20 @@ static hipError_t launch_t(const GemvArgs& a, hipStream_t st) {
   if (ytiles > 2) return hipErrorNotSupported;
   const int G = a.N / RPW;
   int gblocks = (G + WPB - 1) / WPB;
-  const int per_cu = lds <= 72 * 1024 ? 2 : 1;  // blocks the LDS lets share a CU
-  const int cap = 256 * per_cu / ytiles;
+  // persistent: no more blocks than are resident at once (registers, LDS), on every CU
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return hipErrorInvalidDevice;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(&gemv_small_kernel<KCH, RPW, RT, EPI, NORM, F8>),
+          NT, lds) != hipSuccess || per_cu < 1)
+    return hipErrorInvalidConfiguration;
+  const int cap = cus * per_cu / ytiles;
   if (gblocks > cap) gblocks = cap;
   if (ytiles == 2) gblocks = (gblocks + 7) / 8 * 8;
   hipLaunchKernelGGL((gemv_small_kernel<KCH, RPW, RT, EPI, NORM, F8>), dim3(gblocks * ytiles),
@@ -302,6 +374,7 @@ static hipError_t prep_t() {
   X(6, 2, 8, EPI_SILU, true, false) X(6, 2, 4, EPI_SILU, true, false)                      \
   X(16, 1, 4, EPI_RESID, false, false)                                                     \
   X(6, 2, 8, EPI_ARGMAX, true, false) X(6, 2, 4, EPI_ARGMAX, true, false)                  \
+  X(6, 2, 1, EPI_ARGMAX, true, false) X(3, 4, 1, EPI_ARGMAX, true, true)                   \
   X(3, 4, 8, EPI_QKV, true, true) X(3, 4, 4, EPI_QKV, true, true)                          \
   X(3, 2, 8, EPI_RESID, false, true) X(3, 2, 4, EPI_RESID, false, true)                    \
   X(3, 4, 8, EPI_SILU, true, true) X(3, 4, 4, EPI_SILU, true, true)                        \
@@ -322,9 +395,9 @@ hipError_t gemv_small_prepare() {
 hipError_t launch_gemv_small(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   const bool f8 = a.wdtype == WT_FP8;
   const int epc = f8 ? 1024 : 512;
-  if (a.R < 2 || a.R > 8 || a.K % epc) return hipErrorNotSupported;
+  if (a.R < 1 || a.R > 8 || a.K % epc) return hipErrorNotSupported;
   const int kch = a.K / epc;
-  int rt = a.R <= 4 ? 4 : 8;
+  int rt = a.R == 1 ? 1 : a.R <= 4 ? 4 : 8;
   if ((size_t)rt * a.K * 4 > small::LDS_MAX) rt = 4;
 #define MX_L(KCH_, RPW_, RT_, EPI_, NORM_, F8_)                                         \
   if (kch == KCH_ && rt == RT_ && epi == EPI_ && norm == NORM_ && f8 == F8_)              \

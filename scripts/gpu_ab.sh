@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU-box session for a kernel A/B: optional parity tests under engine-option overrides
-# (MORPHEUS_MX_OPT_<key>=<v>, set by the caller), then scripts/ab_decode.py runs (AB1..AB3:
+# (MORPHEUS_MX_OPT_<key>=<v>, set by the caller), then scripts/ab_decode.py runs (AB1..AB6:
 # argument strings).  Each GPU step has its own time limit; a fault / abort / timeout ends it.
 set -u
 OUT=${OUT:-gpurun_out/ab}
@@ -24,4 +24,6 @@ fi
 [ -z "${AB2:-}" ] || step ab2 400 python -u scripts/ab_decode.py $AB2
 [ -z "${AB3:-}" ] || step ab3 400 python -u scripts/ab_decode.py $AB3
 [ -z "${AB4:-}" ] || step ab4 400 python -u scripts/ab_decode.py $AB4
+[ -z "${AB5:-}" ] || step ab5 400 python -u scripts/ab_decode.py $AB5
+[ -z "${AB6:-}" ] || step ab6 400 python -u scripts/ab_decode.py $AB6
 exit 0

@@ -117,6 +117,15 @@ def test_fp8_small_rows_valu_gemv_orpheus_width(n):
     assert _check(cfg, qw, prompts, 6, options={"small_rows": 8}) >= 0.8 * n * 6
 
 
+def test_fp8_small_head_orpheus_width():
+    """Option small_head with e4m3 weights: the one-row fp8 lm_head on the persistent VALU
+    kernel (4 rows per wave, per-row scales), full vocabulary."""
+    cfg = C.OrpheusConfig(layers=2)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=58), cfg)
+    prompt = [int(x) for x in np.random.default_rng(19).integers(1000, 128000, 40)]
+    assert _check(cfg, qw, [prompt], 12, options={"small_head": 1}) >= 9
+
+
 def test_fp8_single_stream_long_context():
     """The default fp8 one-row path over configs[1]'s context range (L 200 -> 1,260): the fp8
     merging o-proj at NSM 2 / 4 / 8 and the 256-position attention past 1,024."""

@@ -182,6 +182,16 @@ def test_decode_parity_orpheus_width_2_layers():
     assert _compare(cfg, w, prompt, 24) >= 20
 
 
+def test_small_head_orpheus_width():
+    """Option small_head: the one-row lm_head on the persistent VALU kernel (rows_small.hip,
+    RT = 1: the normalised row staged once per CU, two row-pair groups in flight per wave),
+    full 156,940-entry vocabulary, penalty over the prompt's repeated ids."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=2)
+    prompt = _orpheus_prompt(12, 7)
+    assert _compare(cfg, w, prompt + prompt[2:8], 16, options={"small_head": 1}) >= 12
+
+
 def _orpheus_prompt(n_text, seed):
     return [128259, 128000] + [int(x) for x in np.random.default_rng(seed).integers(1000, 128000, n_text)] \
         + [128009, 128260, 128261, 128257]
