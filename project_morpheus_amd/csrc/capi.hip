@@ -134,9 +134,9 @@ struct mx_llm {
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
-  int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
-  int small_rows = 0;                // option: largest R on the VALU small-batch GEMV (0 = off)
-  int small_head = 1;                // option: one-row lm_head on the persistent VALU kernel
+  int rows_head_mt = 2;              // option: multi-row lm_head weight rows per wave / 16
+                                     // (2: -22 us at 32 bf16 rows, -28 us at 8 e4m3 rows)
+  int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
@@ -574,8 +574,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_nt_max = x->rows_nt_max;
   g.rows_head_target = x->rows_head_target;
   g.rows_head_mt = x->rows_head_mt;
-  g.small_rows = x->small_rows;
-  g.small_head = x->small_head;
+  g.head_b1 = x->head_b1;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
   g.tickets = x->rows_tickets;
@@ -1003,12 +1002,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_mt") {
     if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_head_mt must be 1 or 2");
     x->rows_head_mt = value;
-  } else if (k == "small_rows") {
-    if (value < 0 || value > 8) MX_FAIL(x, MX_ERR_ARG, "small_rows must be in [0, 8]");
-    x->small_rows = value;
-  } else if (k == "small_head") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "small_head must be 0 or 1");
-    x->small_head = value;
+  } else if (k == "head_b1") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_b1 must be 0 or 1");
+    x->head_b1 = value;
   } else if (k == "rows_frag") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_frag must be 0 or 1");
     x->rows_frag = value;

@@ -982,8 +982,8 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
     const hipError_t e = launch_gemv1(a, epi, norm, st);
     if (e != hipErrorNotSupported || a.att_ml) return e;  // (the merge has no other kernel)
   }
-  if (a.R == 1 && epi == EPI_ARGMAX && a.small_head && !a.force_legacy) {
-    const hipError_t e = launch_gemv_small(a, epi, norm, st);
+  if (a.R == 1 && epi == EPI_ARGMAX && norm && a.head_b1 && !a.force_legacy) {
+    const hipError_t e = launch_head_b1(a, st);
     if (e != hipErrorNotSupported) return e;
   }
   // fp8 single-row lm_head: the grid-stride argmax GEMV with e4m3 weights
@@ -992,11 +992,6 @@ hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   if (a.R == 1 && epi == EPI_ARGMAX && norm && a.wdtype == WT_FP8 && a.K % 1024 == 0) {
     const int blocks = gemv_blocks(a.N, 8, 1, a.max_blocks > 0 ? a.max_blocks : 4096);
     return launch_gemv_t<1, 8, EPI_ARGMAX, true, true>(a, blocks, st);
-  }
-  // a few rows (option small_rows): the VALU small-batch GEMV
-  if (a.R >= 2 && a.R <= a.small_rows && !a.force_legacy) {
-    const hipError_t e = launch_gemv_small(a, epi, norm, st);
-    if (e != hipErrorNotSupported) return e;
   }
   // multi-row steps (and any other fp8 shape) run on the MFMA kernel
   if ((a.R >= 2 && !a.force_legacy) || a.wdtype == WT_FP8) {
@@ -1045,7 +1040,6 @@ hipError_t gemv_prepare(int kmax) {
   if (e == hipSuccess && kmax * 4 + 64 > 64 * 1024)
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<1, 8, EPI_ARGMAX, true, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kmax * 4 + 64);
-  if (e == hipSuccess) e = gemv_small_prepare();
   return e;
 }
 

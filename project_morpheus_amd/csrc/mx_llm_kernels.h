@@ -41,8 +41,7 @@ struct GemvArgs {
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
-  int small_rows;          // 2 <= R <= small_rows: the VALU small-batch GEMV (rows_small.hip; 0 = off)
-  int small_head;          // R = 1 lm_head on the same persistent kernel (one staged row per CU)
+  int head_b1;             // R = 1 lm_head on the persistent kernel (head_b1.hip; 0 = gemv_kernel)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
   const float* rope_sin;
@@ -102,9 +101,8 @@ struct CommitArgs {
 
 hipError_t gemv_prepare(int kmax);
 hipError_t launch_gemv(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-// 1 <= R <= 8 rows on the VALU (rows_small.hip); hipErrorNotSupported outside its shapes
-hipError_t launch_gemv_small(const GemvArgs& a, int epi, bool norm, hipStream_t st);
-hipError_t gemv_small_prepare();
+// R = 1 lm_head + penalty + argmax, persistent (head_b1.hip); hipErrorNotSupported off K = 3072
+hipError_t launch_head_b1(const GemvArgs& a, hipStream_t st);
 namespace v4 {  // multi-row GEMM generation 4 (mx_rows_v4.inc)
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);

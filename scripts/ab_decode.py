@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2,
-            "rows_head_mt": 1, "small_rows": 0, "small_head": 1}
+            "rows_head_mt": 2, "head_b1": 1}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -35,10 +35,8 @@ VARIANTS = {
     "t512": {"rows_target": 512},
     "pw1": {"rows_pw": 1},
     "nw8": {"att_cpw": 1, "att_nw": 8},
-    "hmt2": {"rows_head_mt": 2},
-    "small8": {"small_rows": 8},
-    "shead": {"small_head": 1},
-    "noshead": {"small_head": 0},
+    "hmt1": {"rows_head_mt": 1},
+    "nohead1": {"head_b1": 0},
 }
 
 

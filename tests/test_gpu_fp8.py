@@ -106,24 +106,13 @@ def test_fp8_batched_orpheus_width_8_rows():
     assert _check(cfg, qw, prompts, 6) >= 0.8 * 8 * 6
 
 
-@pytest.mark.parametrize("n", [3, 8])
-def test_fp8_small_rows_valu_gemv_orpheus_width(n):
-    """configs[4]'s 8 fp8 streams on the VALU small-batch GEMV (option small_rows): e4m3
-    weights converted in registers (v_cvt_pk_f32_fp8), per-row scales, packed fp32 FMAs."""
-    cfg = C.OrpheusConfig(layers=2)
-    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=57 + n), cfg)
-    rng = np.random.default_rng(18 + n)
-    prompts = [[int(x) for x in rng.integers(1000, 128000, 5 + 4 * i)] for i in range(n)]
-    assert _check(cfg, qw, prompts, 6, options={"small_rows": 8}) >= 0.8 * n * 6
-
-
-def test_fp8_small_head_orpheus_width():
-    """Option small_head with e4m3 weights: the one-row fp8 lm_head on the persistent VALU
-    kernel (4 rows per wave, per-row scales), full vocabulary."""
+def test_fp8_lm_head_grid_stride_orpheus_width():
+    """Option head_b1 = 0 with e4m3 weights: the grid-stride one-row fp8 lm_head (8 rows per
+    wave) instead of the default persistent head_b1.hip kernel, full vocabulary."""
     cfg = C.OrpheusConfig(layers=2)
     qw = quantize_fp8(synthetic_llm_weights(cfg, seed=58), cfg)
     prompt = [int(x) for x in np.random.default_rng(19).integers(1000, 128000, 40)]
-    assert _check(cfg, qw, [prompt], 12, options={"small_head": 1}) >= 9
+    assert _check(cfg, qw, [prompt], 12, options={"head_b1": 0}) >= 9
 
 
 def test_fp8_single_stream_long_context():

@@ -182,14 +182,14 @@ def test_decode_parity_orpheus_width_2_layers():
     assert _compare(cfg, w, prompt, 24) >= 20
 
 
-def test_small_head_orpheus_width():
-    """Option small_head: the one-row lm_head on the persistent VALU kernel (rows_small.hip,
-    RT = 1: the normalised row staged once per CU, two row-pair groups in flight per wave),
-    full 156,940-entry vocabulary, penalty over the prompt's repeated ids."""
+def test_lm_head_grid_stride_orpheus_width():
+    """The one-row lm_head's other kernel (option head_b1 = 0: the grid-stride gemv_kernel
+    that stages the row per block; the default is the persistent head_b1.hip), full
+    156,940-entry vocabulary, penalty over the prompt's repeated ids."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=2)
     prompt = _orpheus_prompt(12, 7)
-    assert _compare(cfg, w, prompt + prompt[2:8], 16, options={"small_head": 1}) >= 12
+    assert _compare(cfg, w, prompt + prompt[2:8], 16, options={"head_b1": 0}) >= 12
 
 
 def _orpheus_prompt(n_text, seed):
@@ -330,17 +330,6 @@ def test_batched_decode_orpheus_width_64_rows():
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=25)
     assert _compare_rows(cfg, w, _orpheus_prompts(64, 26, 3, 1), 3) >= 0.8 * 64 * 3
-
-
-@pytest.mark.parametrize("n", [2, 5, 8])
-def test_small_rows_valu_gemv_orpheus_width(n):
-    """2 <= R <= 8 rows on the VALU small-batch GEMV (rows_small.hip, option small_rows):
-    one row tile at 2 (RT 4), two tiles of the K = ffn down projection at 5 and 8, the
-    lm_head's penalty/argmax epilogue over 78,470 row pairs, ragged prompts."""
-    cfg = _cfgs("orpheus2")
-    w = synthetic_llm_weights(cfg, seed=60 + n)
-    assert _compare_rows(cfg, w, _orpheus_prompts(n, 61 + n, 4, 3), 6,
-                         options={"small_rows": 8}) >= 0.8 * n * 6
 
 
 @pytest.mark.parametrize("head_target", [2048, 4096])
