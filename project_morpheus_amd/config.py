@@ -127,7 +127,7 @@ SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
 # runs: the same text gives the same audio whatever the batch company or arrival order).
 CONTENT_SEED = env_int("MORPHEUS_MX_CONTENT_SEED", 0)
 # mx_llm_set_option knobs applied to every LlmEngine at creation: MORPHEUS_MX_OPT_<key>=<int>
-# (A/B runs and parity sweeps of a non-default kernel choice, e.g. MORPHEUS_MX_OPT_rows_gen=5).
+# (A/B runs and parity sweeps of a non-default kernel choice, e.g. MORPHEUS_MX_OPT_head_b1=0).
 ENGINE_OPTIONS = {k[len("MORPHEUS_MX_OPT_"):]: int(v) for k, v in os.environ.items()
                   if k.startswith("MORPHEUS_MX_OPT_")}
 # Unit of MxTTSAdapter.pull(n): "bytes" (default; the reference adapters slice bytes,

@@ -14,6 +14,10 @@
 // accumulation (packed v_pk_fma_f32: even / odd k in the two halves), e4m3 converted in
 // registers (v_cvt_pk_f32_fp8, exact).  Measured against the grid-stride gemv_kernel it
 // replaces: step -24 us bf16, -45 us e4m3 (profiles/r04_ab_small_rows_v1_head_options.log).
+// The same persistent design for the one-row gate/up and down projections was slower than
+// gemv1_kernel (+19 / +9 us per step bf16; profiles/r04_b1_persistent_projections_not_kept.log):
+// with 1.5-4 row groups per wave there is little stream to pipeline, and one block per CU
+// hides less latency than gemv1's many one-shot blocks.
 #include "mx_common.h"
 #include "mx_llm_kernels.h"
 
