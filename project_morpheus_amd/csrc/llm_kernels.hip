@@ -953,7 +953,7 @@ static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
 }
 
 // B = 1 path; returns hipErrorNotSupported when the shape has no instantiation.
-// a.rpw (0 = default per epilogue) picks rows per wave: QKV 2, RESID/STORE 1, SILU 2.
+// a.rpw (0 = default per epilogue) picks rows per wave: QKV 2, RESID/STORE 1, SILU 2 (e4m3 4).
 // KCH = 16-byte weight chunks per lane per row: K / 512 (bf16) or K / 1024 (fp8).
 static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   const bool f8 = a.wdtype == WT_FP8;
@@ -961,7 +961,9 @@ static hipError_t launch_gemv1(const GemvArgs& a, int epi, bool norm, hipStream_
   if (a.K % epc) return hipErrorNotSupported;
   const int kch = a.K / epc;
   int rpw = a.rpw;
-  if (rpw == 0) rpw = epi == EPI_QKV ? 2 : epi == EPI_SILU ? 2 : 1;
+  // e4m3 gate/up: 4 rows per wave (12 loads of 16 B per lane, not 6): step 1.106 -> 1.099 ms
+  // at L 600 (profiles/r04_rows_per_wave_ab.log); bf16 is unchanged by it (1.528 / 1.525)
+  if (rpw == 0) rpw = epi == EPI_QKV ? 2 : epi == EPI_SILU ? (f8 ? 4 : 2) : 1;
 #define MX_G1(KCH_, RPW_, EPI_, NORM_)                                                  \
   if (kch == KCH_ && rpw == RPW_ && epi == EPI_ && norm == NORM_ && a.N % RPW_ == 0)     \
     return f8 ? launch_gemv1_t<KCH_, RPW_, EPI_, NORM_, true>(a, st)                    \
