@@ -125,8 +125,10 @@ struct mx_llm {
   int att_cpw_b1 = 0;           // option: chunks per wave, single-row attention (0 = auto)
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
-  int att_nw_b1 = 4, att_nw_batch = 8;
-  int o_merge = 1;  // option: one-row o-proj merges the attention splits (0 = ticket merge)  // options: attention waves per block (4 or 8; measured)
+  int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
+  int o_merge = 1;     // option: one-row o-proj merges the attention splits (0 = ticket merge)
+  int rows_merge = 1;  // option: the same at 2-16 rows (generation-4 o-proj, rows_merge_ok):
+                       // 8 e4m3 rows 1.654 -> 1.637 ms, bf16 8 / 4 / 16 rows unchanged (+-0.1 %)
   int gemv_wpb = 4;
   int rows_lds_pad = 0;              // option: extra LDS KB per multi-row block (occupancy probe)
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
@@ -627,26 +629,29 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.cpw = rs.cpw;
     at.nw = rs.nw;
     at.split_stride = c.max_pos / ATT_S_MIN;
+    // O projection + residual; it merges the attention splits itself (no ticket round trip)
+    // at one row, and at 2-16 rows when its tiling allows (option rows_merge)
+    GemvArgs o{};
+    attach_ws(x, o);
+    o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
+    o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
+    if (x->rows_frag) o.Wf = l.wo_f;
+    o.att_S = 32 * rs.nw * rs.cpw; o.att_stride = at.split_stride; o.att_nsm = rs.nsplit;
+    o.heads = c.heads; o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
     const bool b1_merge = rs.R == 1 && !x->legacy_gemv && x->o_merge && rs.nsplit <= 8;
-    at.no_merge = b1_merge ? 1 : 0;
+    const bool rows_merge = rs.R >= 2 && rs.nsplit > 1 && !x->legacy_gemv && x->rows_merge &&
+                            v4::rows_merge_ok_v4(o);
+    at.no_merge = (b1_merge || rows_merge) ? 1 : 0;
     at.part_ml = x->part_ml; at.part_acc = x->part_acc; at.counter = x->att_cnt;
     at.out = x->att;
     PROF_BEGIN(PK_ATTN);
     e = launch_attention(at, rs.R, rs.max_len, st);
     PROF_END();
     if (e != hipSuccess) break;
-    // O projection + residual
-    GemvArgs o{};
-    attach_ws(x, o);
-    o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
-    o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
-    if (x->rows_frag) o.Wf = l.wo_f;
-    if (b1_merge) {  // the o-projection merges the attention splits (no ticket round trip)
-      if (o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step faster
-                                  // than 1 row per wave (fewer partial re-reads)
-      o.att_ml = x->part_ml; o.att_acc = x->part_acc; o.att_S = 32 * rs.nw * rs.cpw;
-      o.att_stride = at.split_stride; o.att_nsm = rs.nsplit; o.heads = c.heads;
-      o.kv_heads = c.kv_heads; o.row_pos = rs.pos;
+    if (b1_merge || rows_merge) {
+      if (b1_merge && o.rpw == 0) o.rpw = 2;  // 192 blocks of 8 waves: measured 20-37 us/step
+                                              // faster than 1 row per wave (fewer re-reads)
+      o.att_ml = x->part_ml; o.att_acc = x->part_acc;
     }
     PROF_BEGIN(PK_O);
     e = launch_gemv(o, EPI_RESID, false, st);
@@ -1023,6 +1028,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "o_merge") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "o_merge must be 0 or 1");
     x->o_merge = value;
+  } else if (k == "rows_merge") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_merge must be 0 or 1");
+    x->rows_merge = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;

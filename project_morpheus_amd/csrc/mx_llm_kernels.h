@@ -106,6 +106,8 @@ hipError_t launch_head_b1(const GemvArgs& a, hipStream_t st);
 namespace v4 {  // multi-row GEMM generation 4 (mx_rows_v4.inc)
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st);
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
+// the multi-row o-projection can merge the attention splits itself (attn no_merge)
+bool rows_merge_ok_v4(const GemvArgs& o);
 }  // namespace v4
 struct SampleArgs {
   const float* logits;     // [R][V] penalised logits (kept by the lm_head epilogue)

@@ -19,6 +19,8 @@ void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, siz
   }
 }
 
+bool rows_merge_ok_v4(const GemvArgs& o) { return rows_merge_ok(o); }
+
 // R >= 2 rows.  Returns hipErrorNotSupported for shapes the kernel does not cover.
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   if (a.R < 1) return hipErrorNotSupported;

@@ -115,6 +115,17 @@ def test_fp8_lm_head_grid_stride_orpheus_width():
     assert _check(cfg, qw, [prompt], 12, options={"head_b1": 0}) >= 9
 
 
+def test_fp8_batched_orpheus_width_8_rows_split_attention_merged_in_oproj():
+    """configs[4] per GPU at a context where the 8-row attention splits (prompts of 300-335
+    ids, 2 splits of 256): option rows_merge merges the splits in the e4m3 o-projection."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=59), cfg)
+    rng = np.random.default_rng(20)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, 300 + 5 * i)] for i in range(8)]
+    assert _check(cfg, qw, prompts, 4, options={"rows_merge": 1}, max_pos=512,
+                  max_prefill=384) >= 0.8 * 8 * 4
+
+
 def test_fp8_single_stream_long_context():
     """The default fp8 one-row path over configs[1]'s context range (L 200 -> 1,260): the fp8
     merging o-proj at NSM 2 / 4 / 8 and the 256-position attention past 1,024."""

@@ -173,6 +173,48 @@ def test_batched_decode_orpheus_width_32_rows_long_context():
     assert agree >= 0.8 * B * steps
 
 
+@pytest.mark.parametrize("rows_merge", [0, 1])
+def test_batched_decode_orpheus_width_8_rows_split_attention(rows_merge):
+    """configs[3]'s 8-GPU row class (8 rows per GPU) at a context where the multi-row attention
+    splits (a 520-id shared prefix + ragged tails: 3 splits of 256 positions per (row, kv
+    head)): rows_merge 0 merges the splits in the attention (ticket, last arriver), 1 in the
+    generation-4 o-projection's activation staging (attn no_merge)."""
+    from project_morpheus_amd.engine import LlmEngine
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=18)
+    rng = np.random.default_rng(19)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, 520)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, 3 + 5 * r)] for r in range(8)]
+    steps = 8
+    B = len(prompts)
+    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=1024, max_batch=B, max_prefill=576)
+    eng.set_option("rows_merge", rows_merge)
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    toks = [[] for _ in range(B)]
+    logits = [[] for _ in range(B)]
+    for r, p in enumerate(prompts):
+        eng.prefill(r, r, p, 1.1, st)
+    for k in range(steps):
+        if k > 0:
+            eng.decode(B, st)
+        st.synchronize()
+        for r, p in enumerate(prompts):
+            logits[r].append(eng.read_logits(r, st))
+            toks[r].append(int(eng.hist[r, len(p) + k]))
+    eng.close()
+    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=1024)
+    r_logits = L.teacher_forced_rows(ref, prompts, toks, 1.1, shared_prefix=len(prefix))
+    agree = 0
+    for r in range(B):
+        for k in range(steps):
+            np.testing.assert_allclose(logits[r][k], r_logits[r][k].numpy(), atol=LOGIT_TOL,
+                                       rtol=LOGIT_TOL, err_msg=f"row {r} step {k}")
+            assert toks[r][k] == int(np.argmax(logits[r][k]))
+        agree += check_tokens(toks[r], r_logits[r], TIE_MARGIN, what=f"row {r}")
+    assert agree >= 0.8 * B * steps
+
+
 def test_decode_parity_orpheus_width_2_layers():
     """B = 1 at Orpheus widths: the hipGraph step follows the oracle."""
     cfg = _cfgs("orpheus2")
