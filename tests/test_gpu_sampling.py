@@ -24,12 +24,15 @@ LOGIT_TOL = 5e-3
 RACE_MARGIN = 1e-5
 
 
-def _run(cfg, w, rows, steps):
-    """rows: [(prompt, penalty, temperature, top_p, seed)] -> per row (tokens, logits)."""
+def _run(cfg, w, rows, steps, debug_logits=True):
+    """rows: [(prompt, penalty, temperature, top_p, seed)] -> per row (tokens, logits); with
+    debug_logits False the engine keeps logits only for the rows that sample (the product
+    mode) and no logits are read back."""
     from project_morpheus_amd.engine import LlmEngine
     B = len(rows)
     eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=256, max_batch=B, max_prefill=64)
-    eng.enable_logits()
+    if debug_logits:
+        eng.enable_logits()
     st = torch.cuda.Stream()
     out = [([], []) for _ in rows]
     for r, (p, pen, t, tp, sd) in enumerate(rows):
@@ -39,7 +42,8 @@ def _run(cfg, w, rows, steps):
             eng.decode(B, st)
         st.synchronize()
         for r, (p, *_rest) in enumerate(rows):
-            out[r][1].append(eng.read_logits(r, st))
+            if debug_logits:
+                out[r][1].append(eng.read_logits(r, st))
             out[r][0].append(int(eng.hist[r, len(p) + k]))
     eng.close()
     return out
@@ -90,3 +94,18 @@ def test_sampling_single_row_path():
     w = synthetic_llm_weights(cfg, seed=63, std=0.2, norm_jitter=0.5)
     p = [int(x) for x in np.random.default_rng(64).integers(0, cfg.vocab, 9)]
     assert _check(cfg, w, [(p, 1.1, 0.6, 0.8, 99)], 16) >= 15
+
+
+def test_sampling_one_row_hidden_3072_product_mode():
+    """B = 1 at Orpheus width: the persistent lm_head kernel (head_b1.hip) keeps the logits of
+    a sampling row without the debug switch (samp_temp > 0), so the product-mode tokens equal
+    the debug-mode ones, which follow the oracle's draw from the oracle-checked logits."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=65)
+    p = [int(x) for x in np.random.default_rng(66).integers(0, cfg.vocab, 9)]
+    rows = [(p, 1.1, 0.6, 0.9, 4321)]
+    steps = 12
+    assert _check(cfg, w, rows, steps) >= steps - 1
+    debug = _run(cfg, w, rows, steps)[0][0]
+    product = _run(cfg, w, rows, steps, debug_logits=False)[0][0]
+    assert product == debug
