@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
-            "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2,
+            "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
             "rows_head_mt": 2, "head_b1": 1, "rows_merge": 1}
 VARIANTS = {
     "base": {},
@@ -34,6 +34,8 @@ VARIANTS = {
     "t384": {"rows_target": 384},
     "t512": {"rows_target": 512},
     "pw1": {"rows_pw": 1},
+    "f8pw1": {"rows_pw_f8": 1},
+    "t96": {"rows_target": 96},
     "nw8": {"att_cpw": 1, "att_nw": 8},
     "hmt1": {"rows_head_mt": 1},
     "nohead1": {"head_b1": 0},
