@@ -124,15 +124,15 @@ def dry_run(args, rank: int, world: int) -> None:
         dist.destroy_process_group()
 
 
-PMC_RECORD = "r03_pmc_gemv.json" if os.path.exists(
-    os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_pmc_gemv.json")) \
-    else "r02_pmc_gemv.json"
+PMC_RECORD = next((f for f in ("r04_pmc_gemv.json", "r03_pmc_gemv.json", "r02_pmc_gemv.json")
+                   if os.path.exists(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                  "profiles", f))), "r02_pmc_gemv.json")
 
 
 def pmc_traffic(kind, record=PMC_RECORD):
     """HBM bytes per launch of kernel ``kind`` measured by PMC counters in separate rocprofv3
     passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; scripts/pmc_gemv.py and
-    scripts/gpu_pmc_r03.sh, summarised under profiles/); None when that record is absent."""
+    scripts/gpu_pmc_b1.sh, summarised under profiles/); None when that record is absent."""
     path = os.path.join(ROOT, "profiles", record)
     try:
         with open(path) as fh:

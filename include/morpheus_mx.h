@@ -105,7 +105,8 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
 /* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,
- * 1 o-proj, 2 gate/up, 3 down) for `n_rows` rows (1..max_batch), timed over one hipGraph of
+ * 1 o-proj, 2 gate/up, 3 down, 4 the one-row o-proj merging 8 attention splits, 5 lm_head +
+ * penalty + argmax) for `n_rows` rows (1..max_batch), timed over one hipGraph of
  * `reps` sweeps across all layers' weights (as in a decode step); *bytes_out = weight
  * bytes per launch.  Clobbers decode-row state and KV position 0 of the first n_rows
  * slots: only on an idle context. */

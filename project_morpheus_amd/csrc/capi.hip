@@ -930,15 +930,20 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
 // launch (inter-kernel gap in the graph included) and the weight bytes of one launch.
 extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, float* us_out,
                                  double* bytes_out) {
-  if (!x || !us_out || which < 0 || which > 3 || reps < 1) return MX_ERR_ARG;
+  if (!x || !us_out || which < 0 || which > 5 || reps < 1) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
   if (n_rows < 1 || n_rows > c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
   const int H = c.hidden, QD = c.heads * 128;
   MX_TRY(x, hipSetDevice(x->device));
   hipStream_t st = x->cap;
-  if (which == 0) {  // the QKV epilogue writes K/V at (row_slot, row_pos): keep it in range
-    std::vector<int32_t> slots(n_rows), pos(n_rows, 0);
+  if (which == 4 && n_rows != 1) MX_FAIL(x, MX_ERR_ARG, "the merging o-proj is one-row");
+  // 4: the one-row o-proj merging 8 attention splits of 128 positions (row at L = 1,001; the
+  // partial buffers' contents are whatever the last step left: traffic, not values)
+  const int merge_pos = std::min(1000, c.max_pos - 1);
+  if (which == 4 && (merge_pos + 1 + 127) / 128 > 8) MX_FAIL(x, MX_ERR_ARG, "max_pos too small");
+  if (which == 0 || which == 4 || which == 5) {  // keep (row_slot, row_pos) in range
+    std::vector<int32_t> slots(n_rows), pos(n_rows, which == 4 ? merge_pos : 0);
     for (int i = 0; i < n_rows; ++i) slots[i] = i % c.max_slots;
     MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
     MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
@@ -959,14 +964,25 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, flo
     } else if (which == 2) {
       g.W = l.wgu; g.wscale = l.sgu; g.wdtype = c.wdtype; g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
       g.rpw = x->rpw_gu;
-    } else {
+    } else if (which == 3) {
       g.W = l.wd; g.wscale = l.sd; g.wdtype = c.wdtype; g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
+    } else if (which == 4) {
+      g.W = l.wo; g.wscale = l.so; g.wdtype = c.wdtype; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act;
+      g.rpw = x->rpw_o > 0 ? x->rpw_o : 2;
+      g.att_ml = x->part_ml; g.att_acc = x->part_acc; g.att_S = 128;
+      g.att_stride = c.max_pos / ATT_S_MIN; g.att_nsm = (merge_pos + 128) / 128;
+      g.heads = c.heads; g.kv_heads = c.kv_heads; g.row_pos = x->row_pos;
+    } else {  // 5: lm_head + penalty + argmax (the same matrix every launch: 964 MB > MALL)
+      g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype;
+      g.N = c.vocab; g.K = H; g.X = x->h_dec; g.norm_w = x->norm; g.row_slot = x->row_slot;
+      g.seen = x->seen; g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = x->best;
+      g.logits = x->logits; g.logits_all = x->logits_all;
     }
     g.xstride = g.K; g.ystride = g.N;
     return g;
   };
-  const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : EPI_RESID;
-  const bool norm = which == 0 || which == 2;
+  const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : which == 5 ? EPI_ARGMAX : EPI_RESID;
+  const bool norm = which == 0 || which == 2 || which == 5;
   MX_TRY(x, launch_gemv(args(0), epi, norm, st));
   MX_TRY(x, hipStreamSynchronize(st));
   hipGraph_t g = nullptr;

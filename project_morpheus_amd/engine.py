@@ -107,7 +107,8 @@ class LlmEngine:
                                                     C.c_void_p(stream.cuda_stream), ms, n))
         return {k: ms[i] for i, k in enumerate(self.PROFILE_CLASSES)}
 
-    GEMV_KINDS = {"qkv": 0, "o_proj": 1, "gate_up": 2, "down": 3}
+    GEMV_KINDS = {"qkv": 0, "o_proj": 1, "gate_up": 2, "down": 3, "o_proj_merge": 4,
+                  "lm_head": 5}
 
     def bench_gemv(self, which: str, reps: int = 4, n_rows: int = 1):
         """(mean µs per launch, weight bytes per launch) of the ``n_rows``-row decode

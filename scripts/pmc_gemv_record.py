@@ -6,7 +6,11 @@ import json
 import sys
 
 KINDS = {"gemv1_kernel<6, 2, 3,": ("qkv", 31457280), "gemv1_kernel<6, 1, 1, false, 4": ("o_proj", 18874368),
-         "gemv1_kernel<6, 2, 2,": ("gate_up", 100663296), "gemv1_kernel<16, 1, 1,": ("down", 50331648)}
+         "gemv1_kernel<6, 2, 2,": ("gate_up", 100663296), "gemv1_kernel<16, 1, 1,": ("down", 50331648),
+         # the product's one-row o-proj: merges 8 attention splits in its prologue (weights only
+         # counted as algorithmic; the split partials it re-reads are the difference)
+         "gemv1_kernel<6, 2, 1, false, 8, false, 8>": ("o_proj_merge", 18874368),
+         "head_b1_kernel<6, 2, false>": ("lm_head", 156940 * 3072 * 2)}
 
 
 def main():
