@@ -100,9 +100,12 @@ int mx_llm_decode(mx_llm* ctx, int n_rows, void* stream);
  * Synchronises the stream.  Used by bench.py for the roofline of individual kernels. */
 int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_class,
                            int n_classes);
-/* Tuning knobs ("legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "att_cpw",
- * "att_cpw_batch"; see capi.hip).  Drops the
- * captured graphs so the next mx_llm_decode re-captures with the new choice. */
+/* Tuning knobs (capi.hip mx_llm_set_option; unknown keys and out-of-range values fail with
+ * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
+ * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
+ * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
+ * "rows_pw", "rows_pw_f8", "rows_lds_pad".  Drops the captured graphs so the next
+ * mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
 /* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,
  * 1 o-proj, 2 gate/up, 3 down, 4 the one-row o-proj merging 8 attention splits, 5 lm_head +

@@ -1106,8 +1106,6 @@ extern "C" int mx_llm_move_row(mx_llm* x, int dst, int src, void* stream) {
   return MX_OK;
 }
 
-// Diagnostic: copy the last one-launch step's per-block timeline (4 u64 per block: entry,
-// wait done, end on the 100 MHz constant clock, role << 32 | layer) after syncing `stream`.
 extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next_pos) {
   if (!x || !active || !next_pos || row < 0 || row >= x->c.max_batch) return MX_ERR_ARG;
   *active = x->row_active[row];

@@ -223,19 +223,25 @@ static hipError_t launch_t(const GemvArgs& a, hipStream_t st) {
   if (a.N % RPW) return hipErrorNotSupported;
   const int G = a.N / RPW;
   int blocks = (G + WPB - 1) / WPB;
-  // persistent: no more blocks than are resident at once (registers, LDS), on every CU
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+  // persistent: no more blocks than are resident at once (registers, LDS), on every CU.  The
+  // CU count and the occupancy answer are cached per device (a process may drive several
+  // GPUs; each value is idempotent, so concurrent first calls write the same number)
+  constexpr int MAXDEV = 64;
+  static int cus_of[MAXDEV] = {}, per_cu_of[MAXDEV] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return hipErrorInvalidDevice;
+  if (!cus_of[dev]) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       return hipErrorInvalidDevice;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&head_b1_kernel<KCH, RPW, F8>), NT, 0) != hipSuccess ||
+        per_cu < 1)
+      return hipErrorInvalidConfiguration;
+    per_cu_of[dev] = per_cu;
+    cus_of[dev] = cus;
   }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void*>(&head_b1_kernel<KCH, RPW, F8>), NT, 0) != hipSuccess ||
-      per_cu < 1)
-    return hipErrorInvalidConfiguration;
+  const int cus = cus_of[dev], per_cu = per_cu_of[dev];
   if (blocks > cus * per_cu) blocks = cus * per_cu;
   hipLaunchKernelGGL((head_b1_kernel<KCH, RPW, F8>), dim3(blocks), dim3(NT), 0, st, a);
   return hipGetLastError();

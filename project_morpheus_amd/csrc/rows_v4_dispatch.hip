@@ -11,11 +11,16 @@ void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, siz
   for (int cap : {1, 2, 4}) {  // every batch-tile cap option rows_nt_max may pick
     int mt, nt;
     rows_tiles(epi, R, &mt, &nt, cap);
-    // the largest split any rows_target option can ask for (nkc grows with the target)
-    const int nkc = K % 128 ? 1 : rows_nkc(N, K, R, mt, nt, 4096);
-    const size_t tn = (N + 128 * mt - 1) / (128 * mt), tr = (R + 16 * nt - 1) / (16 * nt);
-    *ws_floats = std::max(*ws_floats, nkc > 1 ? tn * tr * nkc * (8 * (size_t)mt * nt * 4 * 64 + 16 * nt) : (size_t)0);
-    *tickets = std::max(*tickets, tn * tr);
+    // the lm_head also runs 32 weight rows per wave (rows_head_mt = 2, batch tiles of 16 / 32)
+    for (int m : {1, 2}) {
+      if (m == 2 && (epi != EPI_ARGMAX || nt > 2)) continue;
+      // the largest split any rows_target option can ask for (nkc grows with the target)
+      const int nkc = K % 128 ? 1 : rows_nkc(N, K, R, m, nt, 4096);
+      const size_t tn = (N + 128 * m - 1) / (128 * m), tr = (R + 16 * nt - 1) / (16 * nt);
+      *ws_floats = std::max(*ws_floats, nkc > 1 ? tn * tr * nkc * (8 * (size_t)m * nt * 4 * 64 + 16 * nt) : (size_t)0);
+      *tickets = std::max(*tickets, tn * tr);
+    }
+    (void)mt;
   }
 }
 

@@ -17,9 +17,18 @@ Out of scope (control plane): text sources, ``/stats``, barge-in 
 admin UI and ``.env`` persistence of ``/config``.
 
     uvicorn project_morpheus_amd.server:app          # or build_app(adapter_cls=...)
+
+The module-level ``app`` differs from the reference server in one observable way unless a
+deployment configures the control plane's stream: without ``orchestrated_stream`` it serves
+plain 4096-byte pulls, so the reference's ladder pull pattern and its per-pull INFO log record
+are absent (the PCM bytes are the same).  ``MORPHEUS_MX_ORCHESTRATED_STREAM=module:callable``
+(e.g. ``harness.orchestrator_contract:orchestrated_pcm_stream``, or the deployment's own
+Orchestrator stream) selects the stream the module-level ``app`` uses.
 """
 from __future__ import annotations
 
+import importlib
+import os
 import struct
 from typing import Optional
 
@@ -182,4 +191,16 @@ def build_app(adapter_cls=None, token_source=_service_tokens, encode=None,
                              Route("/config", update_config, methods=["POST"])])
 
 
-app: Optional[Starlette] = build_app()
+def configured_stream():
+    """The orchestrated stream named by ``MORPHEUS_MX_ORCHESTRATED_STREAM`` ("module:callable"),
+    or None (plain 4096-byte pulls)."""
+    spec = os.environ.get("MORPHEUS_MX_ORCHESTRATED_STREAM", "").strip()
+    if not spec:
+        return None
+    mod, sep, name = spec.partition(":")
+    if not sep or not name:
+        raise ValueError(f"MORPHEUS_MX_ORCHESTRATED_STREAM must be module:callable, got {spec!r}")
+    return getattr(importlib.import_module(mod), name)
+
+
+app: Optional[Starlette] = build_app(orchestrated_stream=configured_stream())

@@ -43,3 +43,60 @@ def b1_attention_shapes(l_lo, l_hi):
 # the default one-row shapes configs[1] reaches past L 512: 5..8 splits of 128 positions
 # (the o-proj's NSM = 8 split merge), then 5 splits of 256 past L 1,024
 LONG_SHAPES = {(4, 1, n) for n in range(5, 9)} | {(4, 2, 5)}
+
+
+# 8 rows whose own split counts differ inside one launch: the o-projection merging
+# at most 2 splits (rows of 1 and 2 splits of 256 positions) and at most 4 (rows of 1..4
+# splits; the launch crosses 768 -> 4 splits at step 9).  A shared 190-id prefix + tails.
+STRADDLE = {"nsm2": ([200, 215, 230, 250, 262, 280, 400, 497], 12),
+            "nsm4": ([200, 260, 330, 480, 520, 600, 700, 760], 12)}
+
+
+def rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=0, max_pos=1024, max_prefill=256,
+                        options=None, wdtype="bf16", ref_w=None, logit_tol=5e-3,
+                        tie_margin=1e-2):
+    """Several streams on their own slots and decode rows, stepped together (the B >= 2
+    path), every row teacher-forced against the oracle (``llama_ref.teacher_forced_rows``;
+    ``shared_prefix`` ids common to every prompt are run once).  ``ref_w``: the oracle's
+    weights when they differ from the engine's (fp8: the dequantised matrices).  Asserts the
+    logits of every (row, step) and the tie-aware tokens; returns the argmax agreements."""
+    import torch
+
+    from oracle import llama_ref as L
+    from project_morpheus_amd.engine import LlmEngine
+
+    from _coverage import check_declared
+    B = len(prompts)
+    check_declared(cfg, [len(p) for p in prompts], steps, wdtype == "fp8", options)
+    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=max_pos, max_batch=B,
+                    max_prefill=max_prefill, wdtype=wdtype)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    toks = [[] for _ in range(B)]
+    logits = [[] for _ in range(B)]
+    for r, p in enumerate(prompts):
+        eng.prefill(r, r, p, 1.1, st)
+    for k in range(steps):
+        if k > 0:
+            eng.decode(B, st)
+        st.synchronize()
+        for r, p in enumerate(prompts):
+            logits[r].append(eng.read_logits(r, st))
+            toks[r].append(int(eng.hist[r, len(p) + k]))
+    eng.close()
+    rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                     kv_heads=cfg.kv_heads, head_dim=cfg.head_dim, ffn=cfg.ffn,
+                     vocab=cfg.vocab, eps=cfg.eps, rope_theta=cfg.rope_theta,
+                     rope_scaling=cfg.rope_scaling)
+    ref = L.LlamaRef(rc, ref_w if ref_w is not None else w, max_pos=max_pos)
+    r_logits = L.teacher_forced_rows(ref, prompts, toks, 1.1, shared_prefix=shared_prefix)
+    agree = 0
+    for r in range(B):
+        for k in range(steps):
+            np.testing.assert_allclose(logits[r][k], r_logits[r][k].numpy(), atol=logit_tol,
+                                       rtol=logit_tol, err_msg=f"row {r} step {k}")
+            assert toks[r][k] == int(np.argmax(logits[r][k]))
+        agree += check_tokens(toks[r], r_logits[r], tie_margin, what=f"row {r}")
+    return agree

@@ -59,3 +59,15 @@ def test_engine_fails_loudly_without_gpu():
     from project_morpheus_amd import _lib
     with pytest.raises(_lib.MxUnavailable):
         _lib.require_gpu()
+
+
+def test_header_option_list_matches_set_option():
+    """include/morpheus_mx.h documents exactly the keys capi.hip mx_llm_set_option accepts."""
+    src = open(os.path.join(ROOT, "project_morpheus_amd", "csrc", "capi.hip")).read()
+    body = src[src.index('extern "C" int mx_llm_set_option'):]
+    body = body[:body.index("unknown option")]
+    accepted = set(re.findall(r'k == "([a-z0-9_]+)"', body))
+    hdr = open(os.path.join(ROOT, "include", "morpheus_mx.h")).read()
+    doc = hdr[hdr.index("Tuning knobs"):hdr.index("int mx_llm_set_option")]
+    documented = set(re.findall(r'"([a-z0-9_]+)"', doc))
+    assert accepted == documented, (accepted - documented, documented - accepted)

@@ -14,7 +14,9 @@ from project_morpheus_amd import config as C
 from project_morpheus_amd.weights import (dequantize_fp8, quantize_fp8,
                                           synthetic_llm_weights)
 
-from _parity import LONG_SHAPES, b1_attention_shapes, check_tokens
+from _coverage import check_declared
+from _parity import (LONG_SHAPES, STRADDLE, b1_attention_shapes, check_tokens,
+                     rows_teacher_forced)
 
 pytestmark = pytest.mark.gpu
 
@@ -29,6 +31,7 @@ def _cfg():
 def _run(cfg, qw, prompts, steps, info=None, options=None, max_pos=512, max_prefill=128):
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
+    check_declared(cfg, [len(p) for p in prompts], steps, True, options)
     eng = LlmEngine(cfg, qw, device=0, max_slots=B, max_pos=max_pos, max_batch=B,
                     max_prefill=max_prefill, wdtype="fp8")
     for k, v in (options or {}).items():
@@ -147,3 +150,29 @@ def test_fp8_single_stream_orpheus_width_long_context():
     steps = 520
     assert LONG_SHAPES <= b1_attention_shapes(601, 600 + steps)
     assert _check(cfg, qw, [prompt], steps, max_pos=1152, max_prefill=640) >= 0.7 * steps
+
+
+def test_fp8_one_row_orpheus_width_split_classes():
+    """The e4m3 one-row merging o-proj at NSM 2 and 4 (gemv1<3,2,1,false,8,true,2|4>): a
+    250-id prompt, L 251..265 crosses 2 -> 3 attention splits of 128 positions."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=79), cfg)
+    prompt = [int(x) for x in np.random.default_rng(80).integers(0, cfg.vocab, 250)]
+    assert b1_attention_shapes(251, 265) == {(4, 1, 2), (4, 1, 3)}
+    assert _check(cfg, qw, [prompt], 16, max_pos=512, max_prefill=256) >= 12
+
+
+@pytest.mark.parametrize("case", ["nsm2", "nsm4"])
+def test_fp8_rows_merge_straddling_splits_orpheus_width(case):
+    """configs[4]'s e4m3 merging o-projection (gemm_rows_kernel<1,1,1,false,3,true,2,NSM>)
+    where the 8 rows of one launch have different split counts (1..2 under NSM 2, 1..4 under
+    NSM 4; the cases of test_gpu_llm.test_rows_merge_straddling_splits_orpheus_width)."""
+    lens, steps = STRADDLE[case]
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=81 if case == "nsm2" else 82), cfg)
+    rng = np.random.default_rng(83)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, 190)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, n - 190)] for n in lens]
+    assert rows_teacher_forced(cfg, qw, prompts, steps, shared_prefix=190, max_pos=1024,
+                               max_prefill=768, wdtype="fp8",
+                               ref_w=dequantize_fp8(qw)) >= 0.8 * 8 * steps

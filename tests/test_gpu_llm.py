@@ -16,7 +16,9 @@ from oracle import llama_ref as L
 from project_morpheus_amd import config as C
 from project_morpheus_amd.weights import synthetic_llm_weights
 
-from _parity import LONG_SHAPES, b1_attention_shapes, check_tokens
+from _coverage import check_declared
+from _parity import (LONG_SHAPES, STRADDLE, b1_attention_shapes, check_tokens,
+                     rows_teacher_forced)
 
 pytestmark = pytest.mark.gpu
 
@@ -39,6 +41,7 @@ def _ref_cfg(c):
 def _run_gpu(cfg, w, prompt, steps, penalty, max_pos=512, options=None, info=None,
              max_prefill=256):
     from project_morpheus_amd.engine import LlmEngine
+    check_declared(cfg, [len(prompt)], steps, False, options)
     eng = LlmEngine(cfg, w, device=0, max_slots=2, max_pos=max_pos, max_batch=1,
                     max_prefill=max_prefill)
     for k, v in (options or {}).items():
@@ -134,43 +137,77 @@ def test_long_context_orpheus_width_default_path():
     assert _compare(cfg, w, prompt, steps, max_pos=1152, max_prefill=640) >= 0.7 * steps
 
 
+def test_one_row_orpheus_width_split_classes():
+    """The one-row merging o-proj at NSM 2 and 4 at Orpheus widths (gemv1<6,2,1,false,8,
+    false,2|4>): a 250-id prompt, L 251..265 crosses 256, i.e. 2 -> 3 attention splits of
+    128 positions."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=73)
+    prompt = [int(x) for x in np.random.default_rng(74).integers(0, cfg.vocab, 250)]
+    assert b1_attention_shapes(251, 265) == {(4, 1, 2), (4, 1, 3)}
+    assert _compare(cfg, w, prompt, 16, max_pos=512, max_prefill=256) >= 12
+
+
+@pytest.mark.parametrize("prompt_len,steps,shapes", [
+    pytest.param(2040, 16, {(4, 2, 8), (4, 4, 5)}, id="2048"),
+    pytest.param(4090, 12, {(4, 4, 8), (8, 4, 5)}, id="4096")])
+def test_long_context_orpheus_width_past_2048_4096(prompt_len, steps, shapes):
+    """The shipped service's context range past configs[1]'s (max_pos 8,192:
+    service.py, llama_local.py:45 n_ctx) at Orpheus widths: the one-row attention
+    crossing 2,048 (256- -> 512-position splits, attn_kernel<3,4,4>) and 4,096 (-> 8-wave
+    1,024-position splits, attn_kernel<3,4,8>), the o-proj merging 5..8 splits."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=75)
+    prompt = [int(x) for x in np.random.default_rng(prompt_len).integers(0, cfg.vocab, prompt_len)]
+    assert b1_attention_shapes(prompt_len + 1, prompt_len + steps - 1) == shapes
+    max_pos = 128 * ((prompt_len + steps + 128) // 128)
+    assert _compare(cfg, w, prompt, steps, max_pos=max_pos, max_prefill=prompt_len) >= 0.7 * steps
+
+
+@pytest.mark.parametrize("prompt_len,shapes", [
+    pytest.param(2040, {(4, 2, 8), (4, 4, 5)}, id="2048"),
+    pytest.param(4090, {(4, 4, 8), (8, 4, 5)}, id="4096"),
+    pytest.param(8150, {(8, 4, 8)}, id="8192")])
+def test_long_context_small_to_max_pos_8192(prompt_len, shapes):
+    """The one-row path to the shipped max_pos 8,192 (small widths): L crossing 2,048 and
+    4,096 and running at 8,151..8,180, every attention shape att_b1_shape picks there
+    ({4,2} -> {4,4} -> {8,4}, up to 8 splits merged in the o-proj)."""
+    cfg = _cfgs("small")
+    w = synthetic_llm_weights(cfg, seed=76, std=0.05, norm_jitter=0.5)
+    prompt = [int(x) for x in np.random.default_rng(prompt_len).integers(0, cfg.vocab, prompt_len)]
+    steps = 30
+    assert b1_attention_shapes(prompt_len + 1, prompt_len + steps - 1) == shapes
+    assert _compare(cfg, w, prompt, steps, max_pos=8192, max_prefill=prompt_len) >= 0.7 * steps
+
+
 def test_batched_decode_orpheus_width_32_rows_long_context():
     """configs[3]'s row class at its context: 32 rows at Orpheus widths, prompts of
     1,405..1,436 ids (a shared 1,400-id prefix + ragged tails), 12 decode steps to L ~1,450
     -- the 8-wave multi-row attention at 6 chunks per wave, one split per (row, kv head)."""
-    from project_morpheus_amd.engine import LlmEngine
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     w = synthetic_llm_weights(cfg, seed=16)
     rng = np.random.default_rng(17)
     prefix = [int(x) for x in rng.integers(0, cfg.vocab, 1400)]
     prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, 5 + r)] for r in range(32)]
     steps = 12
-    B = len(prompts)
-    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=1536, max_batch=B, max_prefill=1440)
-    eng.enable_logits()
-    st = torch.cuda.Stream()
-    toks = [[] for _ in range(B)]
-    logits = [[] for _ in range(B)]
-    for r, p in enumerate(prompts):
-        eng.prefill(r, r, p, 1.1, st)
-    for k in range(steps):
-        if k > 0:
-            eng.decode(B, st)
-        st.synchronize()
-        for r, p in enumerate(prompts):
-            logits[r].append(eng.read_logits(r, st))
-            toks[r].append(int(eng.hist[r, len(p) + k]))
-    eng.close()
-    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=1536)
-    r_logits = L.teacher_forced_rows(ref, prompts, toks, 1.1, shared_prefix=len(prefix))
-    agree = 0
-    for r in range(B):
-        for k in range(steps):
-            np.testing.assert_allclose(logits[r][k], r_logits[r][k].numpy(), atol=LOGIT_TOL,
-                                       rtol=LOGIT_TOL, err_msg=f"row {r} step {k}")
-            assert toks[r][k] == int(np.argmax(logits[r][k]))
-        agree += check_tokens(toks[r], r_logits[r], TIE_MARGIN, what=f"row {r}")
-    assert agree >= 0.8 * B * steps
+    assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=len(prefix), max_pos=1536,
+                               max_prefill=1440) >= 0.8 * 32 * steps
+
+
+@pytest.mark.parametrize("prefix_len", [280, 560, 850])
+def test_batched_decode_orpheus_width_32_rows_attention_chunks(prefix_len):
+    """configs[2] / [3]'s 32-row decode attention at the contexts where its one split per
+    (row, kv head) takes 2 / 3 / 4 chunks of 32 positions per wave (attn_kernel<3,2|3|4,8>,
+    capi.hip att_cpw_auto): a shared prefix of 280 / 560 / 850 ids + ragged tails of 5..36,
+    6 steps."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=60 + prefix_len)
+    rng = np.random.default_rng(prefix_len)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, prefix_len)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, 5 + r)] for r in range(32)]
+    steps = 6
+    assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=prefix_len, max_pos=1024,
+                               max_prefill=prefix_len + 40) >= 0.8 * 32 * steps
 
 
 @pytest.mark.parametrize("rows_merge", [0, 1])
@@ -179,40 +216,35 @@ def test_batched_decode_orpheus_width_8_rows_split_attention(rows_merge):
     splits (a 520-id shared prefix + ragged tails: 3 splits of 256 positions per (row, kv
     head)): rows_merge 0 merges the splits in the attention (ticket, last arriver), 1 in the
     generation-4 o-projection's activation staging (attn no_merge)."""
-    from project_morpheus_amd.engine import LlmEngine
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     w = synthetic_llm_weights(cfg, seed=18)
     rng = np.random.default_rng(19)
     prefix = [int(x) for x in rng.integers(0, cfg.vocab, 520)]
     prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, 3 + 5 * r)] for r in range(8)]
     steps = 8
-    B = len(prompts)
-    eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=1024, max_batch=B, max_prefill=576)
-    eng.set_option("rows_merge", rows_merge)
-    eng.enable_logits()
-    st = torch.cuda.Stream()
-    toks = [[] for _ in range(B)]
-    logits = [[] for _ in range(B)]
-    for r, p in enumerate(prompts):
-        eng.prefill(r, r, p, 1.1, st)
-    for k in range(steps):
-        if k > 0:
-            eng.decode(B, st)
-        st.synchronize()
-        for r, p in enumerate(prompts):
-            logits[r].append(eng.read_logits(r, st))
-            toks[r].append(int(eng.hist[r, len(p) + k]))
-    eng.close()
-    ref = L.LlamaRef(_ref_cfg(cfg), w, max_pos=1024)
-    r_logits = L.teacher_forced_rows(ref, prompts, toks, 1.1, shared_prefix=len(prefix))
-    agree = 0
-    for r in range(B):
-        for k in range(steps):
-            np.testing.assert_allclose(logits[r][k], r_logits[r][k].numpy(), atol=LOGIT_TOL,
-                                       rtol=LOGIT_TOL, err_msg=f"row {r} step {k}")
-            assert toks[r][k] == int(np.argmax(logits[r][k]))
-        agree += check_tokens(toks[r], r_logits[r], TIE_MARGIN, what=f"row {r}")
-    assert agree >= 0.8 * B * steps
+    assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=len(prefix), max_pos=1024,
+                               max_prefill=576, options={"rows_merge": rows_merge}) >= 0.8 * 8 * steps
+
+
+@pytest.mark.parametrize("case", sorted(STRADDLE))
+def test_rows_merge_straddling_splits_orpheus_width(case):
+    """The generation-4 merging o-projection (rows_merge, the default) where the rows of one
+    launch have different split counts: gemm_rows_kernel<1,1,1,false,3,false,2,NSM> with
+    NSM 2 (rows of 1 and 2 splits) and NSM 4 (rows of 1, 2, 3 and 4 splits): the clamped
+    partial loads and the s < ns skip of mx_rows_v4.inc row_merge_load / row_merge_apply."""
+    from _dispatch import ORPHEUS_16K, att_shape, DEFAULTS
+    lens, steps = STRADDLE[case]
+    nsm = {att_shape(ORPHEUS_16K, 8, max(lens) + k, DEFAULTS)[2] for k in range(1, steps)}
+    row_ns = {(n + k + 255) // 256 for n in lens for k in range(1, steps)}
+    assert nsm == ({2} if case == "nsm2" else {3, 4}), nsm
+    assert row_ns == ({1, 2} if case == "nsm2" else {1, 2, 3, 4}), row_ns
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=70 if case == "nsm2" else 71)
+    rng = np.random.default_rng(72)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, 190)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, n - 190)] for n in lens]
+    assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=190, max_pos=1024,
+                               max_prefill=768) >= 0.8 * 8 * steps
 
 
 def test_decode_parity_orpheus_width_2_layers():
@@ -222,6 +254,16 @@ def test_decode_parity_orpheus_width_2_layers():
     prompt = [128259, 128000] + [int(x) for x in np.random.default_rng(3).integers(1000, 128000, 12)] \
         + [128009, 128260, 128261, 128257]
     assert _compare(cfg, w, prompt, 24) >= 20
+
+
+def test_decode_parity_orpheus_width_no_o_merge():
+    """Option o_merge = 0: the one-row attention merges its own splits (ticket, last arriver)
+    and the o-proj is the plain gemv1<6,1,1,false,4,false,0> (the kernel bench.py's roofline
+    section probes for the o-proj class)."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=77)
+    prompt = _orpheus_prompt(12, 78)
+    assert _compare(cfg, w, prompt, 12, options={"o_merge": 0}) >= 9
 
 
 def test_lm_head_grid_stride_orpheus_width():
@@ -269,6 +311,7 @@ def _compare_rows(cfg, w, prompts, steps, penalty=1.1, max_batch=None, options=N
     (the B >= 2 MFMA path); each row teacher-forced against its own oracle run."""
     from project_morpheus_amd.engine import LlmEngine
     B = len(prompts)
+    check_declared(cfg, [len(p) for p in prompts], steps, False, options)
     eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=512, max_batch=max_batch or B,
                     max_prefill=max_prefill)
     for k, v in (options or {}).items():

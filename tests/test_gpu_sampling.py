@@ -29,7 +29,9 @@ def _run(cfg, w, rows, steps, debug_logits=True):
     debug_logits False the engine keeps logits only for the rows that sample (the product
     mode) and no logits are read back."""
     from project_morpheus_amd.engine import LlmEngine
+    from _coverage import check_declared
     B = len(rows)
+    check_declared(cfg, [len(r[0]) for r in rows], steps)
     eng = LlmEngine(cfg, w, device=0, max_slots=B, max_pos=256, max_batch=B, max_prefill=64)
     if debug_logits:
         eng.enable_logits()

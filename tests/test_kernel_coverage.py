@@ -1,0 +1,81 @@
+"""CPU check: every kernel instantiation the bench runs is compared with the oracle by a
+`-m gpu` test (tests/_coverage.py, tests/_dispatch.py).
+
+Three links, each checked mechanically:
+1. the restatement of the library's dispatch (``_dispatch``) predicts the instantiations the
+   hardware ran: every LLM kernel in the committed rocprofv3 summary of a full bench run is
+   in the bench envelope (or is one of the roofline probes);
+2. every instantiation of the envelope (and every probe) is reached by a declared GPU test run;
+3. the declared runs are the ones the GPU tests perform (``check_declared`` inside the test
+   helpers) and every declared test exists.
+"""
+import csv
+import os
+import re
+
+import pytest
+
+from _coverage import GPU_RUNS, bench_envelope, covered_keys, keys_of, probe_keys
+from _dispatch import PREFILL_TAG
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# rocprofv3 --kernel-trace --stats of whole default bench runs (scripts/gpu_full.sh)
+BENCH_TRACES = ["profiles/r04_bench_kernel_stats_final.csv"]
+_LLM = re.compile(r"void mx::((?:v4::gemm_rows|attn|gemv1?|head1::head_b1)_kernel<[^>]*>)"
+                  r"\((?:mx::GemvArgs|mx::AttnArgs)\)")
+
+
+@pytest.fixture(scope="module")
+def envelope():
+    return bench_envelope()
+
+
+def _traced(path):
+    with open(os.path.join(ROOT, path)) as fh:
+        return {m.group(1) for r in csv.DictReader(fh) if (m := _LLM.match(r["Name"]))}
+
+
+def _untag(keys):
+    return {k.replace(PREFILL_TAG, "") for k in keys}
+
+
+@pytest.mark.parametrize("path", BENCH_TRACES)
+def test_restatement_predicts_the_traced_bench(path, envelope):
+    traced = _traced(path)
+    assert len(traced) > 40, traced
+    missing = traced - _untag(envelope) - probe_keys()
+    assert not missing, f"kernels the bench ran that tests/_dispatch.py does not predict: {missing}"
+
+
+def test_every_bench_instantiation_is_parity_tested(envelope):
+    missing = (envelope | probe_keys()) - covered_keys()
+    assert not missing, f"bench instantiations no GPU parity test reaches: {sorted(missing)}"
+
+
+def test_multi_row_decode_attention_is_tested_in_decode(envelope):
+    """The verdict's r04 gap: the multi-row decode attention at 2 / 3 / 4 / 6 chunks per wave
+    (GQA 3) must be reached by DECODE steps of a test, not only by a prefill of the same
+    instantiation (rows on one slot)."""
+    want = {f"attn_kernel<3, {c}, 8>" for c in (1, 2, 3, 4, 6)}
+    assert want <= envelope
+    assert want <= covered_keys()
+
+
+def test_declared_tests_exist():
+    for node in GPU_RUNS:
+        fname, name = node.split("::")
+        base = name.split("[")[0]
+        with open(os.path.join(ROOT, "tests", fname)) as fh:
+            src = fh.read()
+        assert f"def {base}(" in src, node
+        assert keys_of(node), node
+
+
+def test_restatement_knows_the_round4_gaps():
+    """The instantiations round 4's verdict found untested are in the envelope (so link 2
+    covers them)."""
+    env = bench_envelope()
+    for k in ("v4::gemm_rows_kernel<1, 1, 1, false, 3, true, 2, 4>",
+              "v4::gemm_rows_kernel<1, 1, 1, false, 3, false, 2, 2>",
+              "attn_kernel<3, 2, 8>", "attn_kernel<3, 3, 8>", "attn_kernel<3, 4, 8>"):
+        assert k in env, k

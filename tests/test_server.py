@@ -6,6 +6,8 @@ behind the adapter is covered by tests/test_gpu_engine.py and bench.py's http_le
 """
 import struct
 
+import pytest
+
 import numpy as np
 from starlette.testclient import TestClient
 
@@ -80,3 +82,18 @@ def test_ws_tts_frames():
             pass
     assert frames[0] == riff_header()
     assert b"".join(frames[1:]) == b"".join(_pcm_for("Hi there"))
+
+
+def test_module_app_stream_is_configurable(monkeypatch):
+    """MORPHEUS_MX_ORCHESTRATED_STREAM selects the module-level app's orchestrated stream
+    (the default app serves plain pulls, not the reference's ladder + log)."""
+    from project_morpheus_amd import server
+    monkeypatch.delenv("MORPHEUS_MX_ORCHESTRATED_STREAM", raising=False)
+    assert server.configured_stream() is None
+    monkeypatch.setenv("MORPHEUS_MX_ORCHESTRATED_STREAM",
+                       "harness.orchestrator_contract:orchestrated_pcm_stream")
+    from harness.orchestrator_contract import orchestrated_pcm_stream
+    assert server.configured_stream() is orchestrated_pcm_stream
+    monkeypatch.setenv("MORPHEUS_MX_ORCHESTRATED_STREAM", "no_colon")
+    with pytest.raises(ValueError):
+        server.configured_stream()
