@@ -52,9 +52,9 @@ def parse():
                    help="configs[3]: long_read documents (0 skips it)")
     p.add_argument("--step-pos", type=int, default=600,
                    help="position at which the bare decode-step time is measured")
-    p.add_argument("--share-of", type=int, default=8,
+    p.add_argument("--share-of", type=str, default="2,4,8",
                    help="N = 1: also time configs[3]'s largest per-rank share of an N-GPU "
-                        "run on this GPU (0 skips it)")
+                        "run on this GPU, for each N of the comma list ('0' skips it)")
     p.add_argument("--dry-run", action="store_true",
                    help="rank plumbing only: gloo process group, barrier, rank count; no GPU")
     return p.parse_args()
@@ -450,26 +450,38 @@ def run_long_read(args, llm, snac, rank, world, dist):
     audio = sum(len(v) for v in out.values()) / 24000.0
     mine = S.assign(jobs, world)
     share = None
-    if world == 1 and args.share_of > 1:
-        # strong-scaling forecast measured on hardware: the most loaded rank of an
-        # args.share_of-GPU run (assign() is deterministic, so this is exactly its job list)
-        # served alone on this GPU
-        plan = S.assign(jobs, args.share_of)
-        r_max = max(range(args.share_of), key=lambda r: (sum(jobs[i].cost for i in plan[r]), -r))
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        pcm = synthesize([jobs[i] for i in plan[r_max]])
-        torch.cuda.synchronize()
-        t_share = time.perf_counter() - t0
-        ideal = wall / args.share_of
-        share = {"share_of": args.share_of, "rank": r_max, "jobs": len(plan[r_max]),
-                 "wall_s": round(t_share, 3),
-                 "audio_seconds": round(sum(len(p) for p in pcm) / 2 / 24000.0, 2),
-                 "predicted_value": round(audio / t_share, 3),
-                 "predicted_strong_scaling_eff": round(ideal / t_share, 4),
-                 "note": ("the most loaded rank's jobs of an N-GPU run timed alone on one GPU; "
-                          "predicted value = all documents' audio / that wall (the rank-0 "
-                          "gather and stitch excluded)")}
+    shares = [int(x) for x in str(args.share_of).split(",") if x.strip() and int(x) > 1]
+    if world == 1 and shares:
+        # strong-scaling forecast measured on hardware: the most loaded rank of an N-GPU run
+        # (assign() is deterministic, so this is exactly its job list) served alone on this
+        # GPU, for every N asked; beside it the HBM-roofline bound of the same split
+        # (sharding.scaling_bound: one GPU batches up to 32 streams per weight read, N GPUs
+        # only 64 / N each, so even perfect kernels cannot scale this fixed workload linearly)
+        cfg = llm.cfg
+        share = {}
+        for n_share in shares:
+            plan = S.assign(jobs, n_share)
+            r_max = max(range(n_share), key=lambda r: (sum(jobs[i].cost for i in plan[r]), -r))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pcm = synthesize([jobs[i] for i in plan[r_max]])
+            torch.cuda.synchronize()
+            t_share = time.perf_counter() - t0
+            bound = S.scaling_bound(jobs, n_share, cfg.step_weight_bytes(),
+                                    cfg.kv_bytes_per_position(), max_rows=llm.max_batch)
+            share[str(n_share)] = {
+                "share_of": n_share, "rank": r_max, "jobs": len(plan[r_max]),
+                "wall_s": round(t_share, 3),
+                "audio_seconds": round(sum(len(p) for p in pcm) / 2 / 24000.0, 2),
+                "predicted_value": round(audio / t_share, 3),
+                "predicted_strong_scaling_eff": round(wall / n_share / t_share, 4),
+                "roofline_eff_bound": bound["efficiency_bound"]}
+        share["note"] = ("per N: the most loaded rank's jobs of an N-GPU run timed alone on one "
+                         "GPU; predicted value = all documents' audio / that wall (the rank-0 "
+                         "gather and stitch excluded); roofline_eff_bound = the strong-scaling "
+                         "efficiency this fixed 64-job split allows with every GPU at its HBM "
+                         "roofline (sharding.scaling_bound: 32 rows per weight read on 1 GPU, "
+                         "64 / N on N GPUs)")
     return {"workload": (f"configs[3]: long_read, {len(docs)} documents x ~3000 chars (seed 5) "
                          f"-> {len(jobs)} <=1000-char batches x {args.max_tokens} tokens, "
                          f"sharded over {world} GPU(s), continuous batching per GPU, ordered "

@@ -153,3 +153,43 @@ def long_read_documents(n_docs: int = 16, n_chars: int = 3000, seed: int = 5) ->
             total += len(s) + 1
         docs.append(" ".join(words))
     return docs
+
+
+def roofline_wall(jobs: Sequence[Job], weight_bytes: int, kv_bytes_per_pos: int,
+                  max_rows: int = 32, hbm_bps: float = 8e12) -> float:
+    """HBM-roofline time for ONE GPU to serve ``jobs`` through the continuous-batching loop:
+    jobs are admitted in order, at most ``max_rows`` at a time; every prefill streams the
+    weights once, and every decode step streams them once plus the KV cache of each live row
+    (``kv_bytes_per_pos`` per position).  A lower bound of the wall (it ignores compute,
+    launch gaps and the SNAC work), used to bound strong scaling (``scaling_bound``)."""
+    live: List[List[int]] = []          # [position, tokens left]
+    pending = [(len(j.prompt_ids), j.max_tokens) for j in jobs]
+    total = 0.0
+    while pending or live:
+        while pending and len(live) < max_rows:
+            p, t = pending.pop(0)
+            total += weight_bytes
+            live.append([p, t - 1])     # the prefill picks the first token
+        live = [r for r in live if r[1] > 0]
+        if not live:
+            continue
+        total += weight_bytes + kv_bytes_per_pos * sum(r[0] + 1 for r in live)
+        for r in live:
+            r[0] += 1
+            r[1] -= 1
+    return total / hbm_bps
+
+
+def scaling_bound(jobs: Sequence[Job], world: int, weight_bytes: int, kv_bytes_per_pos: int,
+                  max_rows: int = 32) -> dict:
+    """Strong-scaling bound of a FIXED job list spread over ``world`` GPUs by ``assign``,
+    every GPU at its HBM roofline: efficiency = T(1 GPU) / (world x T(most loaded rank)).
+    One GPU batches up to ``max_rows`` streams per weight read; ``world`` GPUs each batch
+    only their share, so the weight bytes per token grow with ``world`` and the bound falls
+    below 1 even with perfect kernels."""
+    t1 = roofline_wall(jobs, weight_bytes, kv_bytes_per_pos, max_rows)
+    plan = assign(jobs, world)
+    tn = max(roofline_wall([jobs[i] for i in mine], weight_bytes, kv_bytes_per_pos, max_rows)
+             for mine in plan)
+    return {"world": world, "t1_roofline_s": round(t1, 4), "tn_roofline_s": round(tn, 4),
+            "efficiency_bound": round(t1 / (world * tn), 4)}

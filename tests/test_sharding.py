@@ -128,3 +128,33 @@ def test_gloo_world2_gather_matches_single_rank(tmp_path, crossfade_ms):
     assert sorted(got) == sorted(exp)
     for d in exp:
         np.testing.assert_array_equal(got[d], exp[d])
+
+
+def test_scaling_bound_of_the_long_read_split():
+    """configs[3]'s fixed 64-job workload: with every GPU at its HBM roofline, 1 GPU batches
+    32 streams per weight read and N GPUs 64 / N, so strong scaling is bounded below linear
+    (bench.py reports this bound beside the measured per-N rank-share forecast)."""
+    from project_morpheus_amd import config as C
+    from project_morpheus_amd.tokenizer import Tokenizer
+    cfg = C.OrpheusConfig()
+    jobs = S.plan_jobs(S.long_read_documents(16, 3000, seed=5), Tokenizer(None).encode,
+                       "tara", 1200)
+    assert len(jobs) == 64
+    b = {n: S.scaling_bound(jobs, n, cfg.step_weight_bytes(), cfg.kv_bytes_per_position())
+         for n in (1, 2, 4, 8)}
+    assert b[1]["efficiency_bound"] == 1.0
+    assert 1.0 >= b[2]["efficiency_bound"] > b[4]["efficiency_bound"] > b[8]["efficiency_bound"]
+    assert 0.25 < b[8]["efficiency_bound"] < 0.45
+    # the roofline wall of one GPU: 2 waves of 32 rows x 1,200 steps of >= 6.6 GB each
+    assert b[1]["t1_roofline_s"] > 2 * 1200 * cfg.step_weight_bytes() / 8e12
+
+
+def test_roofline_wall_counts_prefills_and_kv():
+    j = [S.Job(0, i, "x", prompt_ids=[1] * 10, max_tokens=3) for i in range(3)]
+    W, kv = 100, 1
+    # 3 prefills (3 W) + 2 decode steps over 3 rows at positions 10 -> 11, 11 -> 12
+    want = 3 * W + (W + 3 * 11) + (W + 3 * 12)
+    assert abs(S.roofline_wall(j, W, kv, max_rows=32, hbm_bps=1.0) - want) < 1e-9
+    # max_rows 2: rows 0, 1 first (2 prefills, 2 steps), then row 2 (1 prefill, 2 steps)
+    want2 = 2 * W + (W + 2 * 11) + (W + 2 * 12) + W + (W + 11) + (W + 12)
+    assert abs(S.roofline_wall(j, W, kv, max_rows=2, hbm_bps=1.0) - want2) < 1e-9
