@@ -96,7 +96,8 @@ int mx_llm_prefill(mx_llm* ctx, int slot, int row, const int32_t* ids_host, int 
 int mx_llm_decode(mx_llm* ctx, int n_rows, void* stream);
 /* Same step launched eagerly (no graph) with HIP events around every launch; adds the
  * elapsed milliseconds per launch class to ms_by_class[k] (k < n_classes; classes:
- * 0 qkv, 1 attention, 2 o-proj, 3 gate/up, 4 down, 5 lm_head+argmax, 6 commit).
+ * 0 qkv, 1 attention, 2 o-proj, 3 gate/up, 4 down, 5 lm_head+argmax, 6 commit, 7 the
+ * persistent engine launch when option b1_engine is on).
  * Synchronises the stream.  Used by bench.py for the roofline of individual kernels. */
 int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_class,
                            int n_classes);
@@ -104,8 +105,9 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
- * "rows_pw", "rows_pw_f8", "rows_lds_pad".  Drops the captured graphs so the next
- * mx_llm_decode re-captures with the new choice. */
+ * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
+ * launch, engine_b1.hip), "engine_slots" (its LDS ring depth, set before b1_engine).  Drops
+ * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
 /* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,
  * 1 o-proj, 2 gate/up, 3 down, 4 the one-row o-proj merging 8 attention splits, 5 lm_head +

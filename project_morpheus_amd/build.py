@@ -15,9 +15,9 @@ LIB = os.path.join(HERE, "libmorpheus_mx.so")
 OBJ_DIR = os.path.join(CSRC, "build")  # per-translation-unit objects (git-ignored)
 SOURCES = ["capi.hip", "llm_kernels.hip", "rows_v4_dispatch.hip", "rows_v4_qkv.hip",
            "rows_v4_resid.hip", "rows_v4_silu.hip", "rows_v4_head.hip", "head_b1.hip",
-           "sample_kernels.hip", "snac_kernels.hip"]
+           "sample_kernels.hip", "snac_kernels.hip", "engine_b1.hip"]
 HEADERS = ["mx_common.h", "mx_llm_kernels.h", "mx_snac_kernels.h", "mx_rows_common.h",
-           "mx_rows_v4.inc"]
+           "mx_rows_v4.inc", "mx_engine.h"]
 ARCH = os.environ.get("MORPHEUS_MX_ARCH", "gfx950")
 
 

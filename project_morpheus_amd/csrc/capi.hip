@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/morpheus_mx.h"
+#include "mx_engine.h"
 #include "mx_llm_kernels.h"
 #include "mx_snac_kernels.h"
 
@@ -141,6 +142,15 @@ struct mx_llm {
   int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
+  // persistent one-row engine (engine_b1.hip): option b1_engine runs the layers of a
+  // one-row decode step as one launch (engine_slots = its LDS ring depth)
+  int b1_engine = 0, engine_slots = 7, engine_grid = 0;
+  uint2 *g_qkv = nullptr, *g_att = nullptr, *g_h1 = nullptr, *g_act = nullptr, *g_h2 = nullptr;
+  float* eng_part = nullptr;
+  int* eng_tickets = nullptr;
+  uint32_t* eng_epoch = nullptr;
+  int* eng_status_h = nullptr;  // host-mapped status word of the last engine launches
+  int* eng_status_d = nullptr;
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
@@ -278,6 +288,17 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   A(x->samp_top_p, slots);
   A(x->samp_seed, 2 * slots);
   A(x->logits, (size_t)c.max_batch * c.vocab);
+  {  // engine hand-off granules and attention partials (small: ~1 MB)
+    const size_t QD = (size_t)c.heads * 128, KVD = (size_t)c.kv_heads * 128;
+    A(x->g_qkv, QD + 2 * KVD);
+    A(x->g_att, QD);
+    A(x->g_h1, c.hidden);
+    A(x->g_act, c.ffn);
+    A(x->g_h2, c.hidden);
+    A(x->eng_part, (size_t)c.kv_heads * ((c.max_pos + 127) / 128) * (c.heads / c.kv_heads) * 130);
+    A(x->eng_tickets, (size_t)c.layers * c.kv_heads);
+    A(x->eng_epoch, 2);
+  }
 #undef A
   if (c.tied && !f8) x->lm = x->embed;
   if (e != hipSuccess) {
@@ -296,6 +317,15 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   }
   x->hist_host = (int32_t*)hh;
   x->hist_dev = (int32_t*)hd;
+  if (mx_host_alloc(64, &hh, &hd) != MX_OK) {
+    g_err = "host status alloc failed";
+    (void)hipHostFree(x->hist_host);
+    for (void* p : x->allocs) (void)hipFree(p);
+    delete x;
+    return MX_ERR_OOM;
+  }
+  x->eng_status_h = (int*)hh;
+  x->eng_status_d = (int*)hd;
   e = hipMemset(x->kcache, 0, x->kv_layer_elems * c.layers * 2);
   if (e == hipSuccess) e = hipMemset(x->vcache, 0, x->kv_layer_elems * c.layers * 2);
   if (e == hipSuccess) e = hipMemset(x->best, 0, c.max_batch * 8);
@@ -305,6 +335,17 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
   if (e == hipSuccess) e = hipMemset(x->h_dec, 0, (size_t)c.max_batch * c.hidden * 4);
   if (e == hipSuccess) e = hipMemset(x->samp_temp, 0, slots * 4);  // greedy everywhere
   if (e == hipSuccess) e = hipMemset(x->samp_seed, 0, slots * 8);
+  if (e == hipSuccess) {
+    const size_t QD = (size_t)c.heads * 128, KVD = (size_t)c.kv_heads * 128;
+    const uint32_t ep[2] = {1u, 0u};  // granule tags of epoch 0 would match zeroed buffers
+    e = hipMemset(x->g_qkv, 0, (QD + 2 * KVD) * 8);
+    if (e == hipSuccess) e = hipMemset(x->g_att, 0, QD * 8);
+    if (e == hipSuccess) e = hipMemset(x->g_h1, 0, (size_t)c.hidden * 8);
+    if (e == hipSuccess) e = hipMemset(x->g_act, 0, (size_t)c.ffn * 8);
+    if (e == hipSuccess) e = hipMemset(x->g_h2, 0, (size_t)c.hidden * 8);
+    if (e == hipSuccess) e = hipMemset(x->eng_tickets, 0, (size_t)c.layers * c.kv_heads * 4);
+    if (e == hipSuccess) e = hipMemcpy(x->eng_epoch, ep, 8, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) {
     std::vector<float> ones(slots, 1.0f);
     e = hipMemcpy(x->penalty, ones.data(), slots * 4, hipMemcpyHostToDevice);
@@ -584,7 +625,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
 }
 
 // Optional per-launch timing (eager runs only): prof->ev[k] brackets launch class k.
-enum { PK_QKV = 0, PK_ATTN, PK_O, PK_GU, PK_DOWN, PK_HEAD, PK_COMMIT, PK_N };
+enum { PK_QKV = 0, PK_ATTN, PK_O, PK_GU, PK_DOWN, PK_HEAD, PK_COMMIT, PK_ENGINE, PK_N };
 struct Prof {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
   void begin(int k, hipStream_t st) {
@@ -723,14 +764,39 @@ static bool any_samples(const mx_llm* x, int n_rows) {
   return false;
 }
 
+static EngineArgs engine_args(const mx_llm* x) {
+  const auto& c = x->c;
+  EngineArgs a{};
+  a.wqkv = x->wqkv_all; a.wo = x->wo_all; a.wgu = x->wgu_all; a.wd = x->wd_all;
+  a.sqkv = x->sqkv_all; a.so = x->so_all; a.sgu = x->sgu_all; a.sd = x->sd_all;
+  a.attn_norm = x->attn_norm_all; a.mlp_norm = x->mlp_norm_all;
+  a.rope_cos = x->rope_cos; a.rope_sin = x->rope_sin;
+  a.kcache = x->kcache; a.vcache = x->vcache; a.kv_layer_elems = x->kv_layer_elems;
+  a.row_slot = x->row_slot; a.row_pos = x->row_pos; a.h = x->h_dec;
+  a.g_qkv = x->g_qkv; a.g_att = x->g_att; a.g_h1 = x->g_h1; a.g_act = x->g_act; a.g_h2 = x->g_h2;
+  a.part = x->eng_part; a.tickets = x->eng_tickets; a.epoch = x->eng_epoch; a.status = x->eng_status_d;
+  a.layers = c.layers; a.H = c.hidden; a.heads = c.heads; a.kv_heads = c.kv_heads; a.F = c.ffn;
+  a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
+  a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps;
+  a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
+  return a;
+}
+
 static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, bool sample,
                                  hipStream_t st, Prof* prof) {
   const auto& c = x->c;
-  const int nw = att_nw_of(x, n_rows, max_len);
-  const int S = 32 * nw * cpw;
-  RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw, nw,
-            (max_len + S - 1) / S};
-  hipError_t e = enqueue_layers(x, rs, st, prof);
+  hipError_t e = hipSuccess;
+  if (n_rows == 1 && x->b1_engine) {  // every layer in one persistent launch
+    PROF_BEGIN(PK_ENGINE);
+    e = launch_engine_b1(engine_args(x), x->engine_grid, st);
+    PROF_END();
+  } else {
+    const int nw = att_nw_of(x, n_rows, max_len);
+    const int S = 32 * nw * cpw;
+    RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw, nw,
+              (max_len + S - 1) / S};
+    e = enqueue_layers(x, rs, st, prof);
+  }
   PROF_BEGIN(PK_HEAD);
   if (e == hipSuccess)
     e = enqueue_head(x, x->h_dec, x->row_slot, x->row_pos, n_rows, x->best, sample, st);
@@ -811,13 +877,19 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
+  if (x->eng_status_h && __atomic_load_n(x->eng_status_h, __ATOMIC_ACQUIRE)) {
+    const int s = __atomic_exchange_n(x->eng_status_h, 0, __ATOMIC_ACQ_REL);
+    MX_FAIL(x, MX_ERR_HIP, "persistent engine launch gave up (status " + std::to_string(s) +
+                               "): a hand-off timed out; the step's outputs are invalid");
+  }
   // one graph per (row count, attention split count): kernels read positions from device
-  // memory; the split count only sizes the attention grid
+  // memory; the split count only sizes the attention grid (the engine sizes its own)
+  const bool engine = n_rows == 1 && x->b1_engine;
   const int ml = decode_max_len(x, n_rows);
-  const int cpw = att_cpw_auto(x, n_rows, ml);
-  const int nw = att_nw_of(x, n_rows, ml);
+  const int cpw = engine ? 1 : att_cpw_auto(x, n_rows, ml);
+  const int nw = engine ? 1 : att_nw_of(x, n_rows, ml);
   const int S = 32 * cpw * nw;
-  const int nsplit = (ml + S - 1) / S;
+  const int nsplit = engine ? 0 : (ml + S - 1) / S;
   // (chunks and waves are part of the key: one nsplit can come from several shapes; so is
   // whether any row samples: all-greedy graphs have no sampler node)
   const bool sample = any_samples(x, n_rows);
@@ -1023,6 +1095,29 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_mt") {
     if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_head_mt must be 1 or 2");
     x->rows_head_mt = value;
+  } else if (k == "b1_engine" || k == "engine_slots") {
+    const bool en = k == "b1_engine" ? value != 0 : x->b1_engine != 0;
+    const int slots = k == "engine_slots" ? value : x->engine_slots;
+    if (k == "b1_engine" && value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine must be 0 or 1");
+    if (slots < 3 || slots > 8 || engine_lds_bytes(slots, x->c.hidden, x->c.ffn) > 160 * 1024)
+      MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3..8 and fit the CU's 160 KB of LDS");
+    if (en) {
+      const auto& c = x->c;
+      MX_TRY(x, hipSetDevice(x->device));
+      int cus = 0, per_cu = 0;
+      MX_TRY(x, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, x->device));
+      if (c.hidden % 1024 || c.ffn % 1024 || c.heads * 128 != c.hidden || c.layers > 31 ||
+          c.heads / c.kv_heads > 4 || (c.hidden + cus - 1) / cus > 32)
+        MX_FAIL(x, MX_ERR_ARG, "b1_engine: model shape outside the engine's (hidden = heads x 128, "
+                               "multiples of 1024, <= 31 layers, GQA <= 4)");
+      EngineArgs ea = engine_args(x);
+      ea.ring_slots = slots;
+      MX_TRY(x, engine_per_cu(ea, &per_cu));
+      if (per_cu < 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine: a workgroup does not fit one CU");
+      x->engine_grid = cus;  // one per CU, all co-resident (every wait is also time-bounded)
+    }
+    x->engine_slots = slots;
+    x->b1_engine = en ? 1 : 0;
   } else if (k == "head_b1") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_b1 must be 0 or 1");
     x->head_b1 = value;
@@ -1143,6 +1238,7 @@ extern "C" void mx_llm_destroy(mx_llm* x) {
   if (x->cap) (void)hipStreamDestroy(x->cap);
   for (void* p : x->allocs) (void)hipFree(p);
   if (x->hist_host) (void)hipHostFree(x->hist_host);
+  if (x->eng_status_h) (void)hipHostFree(x->eng_status_h);
   delete x;
 }
 

@@ -1,0 +1,782 @@
+// Persistent one-row decode engine (option b1_engine): every layer of one B = 1 decode step
+// in ONE launch, so the HBM weight stream never stops at a layer's dependency edges.
+//
+// Replaces the per-kernel hipGraph step (qkv -> attention -> o-proj -> gate/up -> down, 140
+// launches per step) for the single-stream decode of vLLM's engine
+// (Orpheus-TTS/orpheus_tts_pypi/orpheus_tts/engine_class.py:117, CUDA-graph decode) and
+// llama.cpp (Morpheus_Client/tts_engine/llama_local.py:77).  Design: MI355X_MICROARCH.md
+// "Persistent kernels" price list, rows ldsdma-fill / nt-weights / engine-vs-launches.
+//
+// One workgroup per CU (grid = CU count, all co-resident), 5 waves:
+//   * wave 0 = LOADER: walks the CU's static weight schedule (every layer: its rows of wqkv,
+//     wo, wgu, wd, contiguous row ranges) and streams it into an LDS ring of 16 KB slots with
+//     LDS-DMA (global_load_lds_dwordx4 nt: one 1 KB wave instruction per 64 lanes x 16 B),
+//     two slots in flight, publishing a slot (LDS word = sequence number) once its loads have
+//     landed (counted vmcnt).  It never waits on data, only on a free ring slot, so the
+//     stream runs on across every dependency edge of the layer.
+//   * waves 1..4 = CONSUMERS: gather each phase's input vector, compute their slots (slot k
+//     -> wave k mod 4) from LDS, and publish outputs.
+// Cross-CU hand-offs are 8-byte granules {fp32 value, u32 tag}, one write-through (sc1) store
+// each, read back with sc1 loads until every tag matches (MI355X_MICROARCH.md granule rows; no
+// counters, no fences).  tag = epoch << 8 | layer << 3 | phase; the epoch advances once per
+// launch (the last workgroup to finish bumps it), so a granule of an earlier step never
+// matches.
+//
+// Phases per layer (each CU owns a contiguous row range of every matrix):
+//   QKV  : gather h (layer input), RMSNorm folded (y = W(x*w) * rsqrt(mean x^2 + eps)); rows of
+//          the packed wqkv -> RoPE -> q / k / v granules (+ the bf16 K/V cache at pos).
+//   ATTN : items (kv head, split of 128 positions) on spread CUs: the cached positions [0, L-1)
+//          on bf16 MFMA exactly as attn_kernel (three bf16 parts of q and p), position L-1 from
+//          the k / v granules (bf16-rounded, as the cache will hold it); split partials merged
+//          by the last arriving split (ticket), which publishes the attention output granules.
+//   O    : gather att; rows of wo; h1 = h + y granules.
+//   GU   : gather h1 (RMSNorm); rows of wgu (gate/up interleaved); silu(g) u granules.
+//   DOWN : gather act; rows of wd; h2 = h1 + y granules (the next layer's input); the last
+//          layer also stores h2 to the decode row's hidden state for the lm_head launch.
+// Every wait is bounded (100 MHz realtime clock): a stuck hand-off sets *status and every wave
+// leaves, so a launch always drains.
+#include "mx_common.h"
+#include "mx_llm_kernels.h"
+#include "mx_engine.h"
+
+namespace mx {
+namespace eng {
+
+constexpr int NC = 4;                // consumer waves
+constexpr int NT = 64 * (NC + 1);    // workgroup threads
+constexpr int SLOT = 16384;          // ring slot bytes
+constexpr int DEPTH = 2;             // ring slots the loader keeps in flight
+constexpr int SL = 128;              // attention split length (positions; 4 waves x 32)
+enum { PH_QKV = 0, PH_ATT = 1, PH_H1 = 2, PH_ACT = 3, PH_H2 = 4 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_cvoid;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+// ---- granules (8 bytes: value, tag), write-through stores / loads -------------------------
+__device__ __forceinline__ void gput(uint2* g, int i, float v, uint32_t tag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(v), tag}, r, i * 8, 0, 16);
+}
+__device__ __forceinline__ u32x4v gget2(const uint2* g, int i) {  // granules i, i + 1
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(g), 0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, i * 8, 0, 16);
+}
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- LDS words shared by the waves of the workgroup ------------------------------------
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct Ctl {           // LDS control block
+  int ready[8];        // ring position -> sequence number of the slot it holds (k + 1)
+  int freed[8];        // ring position -> sequence number of the slot consumed from it
+  int bar;             // consumer barrier arrivals (monotonic)
+  int abort_;          // a wave of this workgroup gave up
+  int last;            // attention ticket: this CU merges
+  int pad;
+  float ss[NC];        // per-wave partial sums of squares
+  float res1[32], res2[32];  // this CU's residual slice (o-proj / down rows)
+};
+
+struct Clock {
+  uint64_t deadline;
+  __device__ bool expired() const { return __builtin_amdgcn_s_memrealtime() > deadline; }
+};
+
+// one matrix phase of the static weight schedule, for this CU
+struct Ph {
+  const uint8_t* W;    // layer 0 base
+  size_t layer_bytes;  // bytes per layer
+  int r0, r1;          // this CU's rows
+  int rps, ips;        // rows per slot, 1 KB instructions per slot
+  int rowbytes, nslots;
+  int N;
+};
+
+__device__ __forceinline__ Ph make_ph(const void* W, int N, int K, int esz, int G, int c,
+                                      bool pair) {
+  Ph p;
+  p.W = static_cast<const uint8_t*>(W);
+  p.N = N;
+  p.rowbytes = K * esz;
+  p.layer_bytes = (size_t)N * p.rowbytes;
+  int per = (N + G - 1) / G;
+  if (pair) per = (per + 1) & ~1;
+  p.r0 = min(N, c * per);
+  p.r1 = min(N, p.r0 + per);
+  p.rps = SLOT / p.rowbytes;
+  if (pair) p.rps &= ~1;
+  p.ips = p.rps * p.rowbytes / 1024;
+  p.nslots = (p.r1 - p.r0 + p.rps - 1) / p.rps;
+  return p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// vmcnt <= n, for the in-flight counts the schedule produces (slots of 12 / 16 instructions,
+// DEPTH newer slots); any other n waits for the largest listed count below it
+__device__ __forceinline__ void wait_vm_n(int n) {
+  if (n >= 32) wait_vm<32>();
+  else if (n >= 28) wait_vm<28>();
+  else if (n >= 24) wait_vm<24>();
+  else if (n >= 16) wait_vm<16>();
+  else if (n >= 12) wait_vm<12>();
+  else wait_vm<0>();
+}
+
+// ---------------------------------------------------------------------------------------
+// consumer helpers
+// ---------------------------------------------------------------------------------------
+// consumer-only barrier (the loader never joins): monotonic arrival count in LDS
+__device__ __forceinline__ bool cbar(Ctl* ctl, int& gen, const Clock& clk, int* status) {
+  gen += NC;
+  asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(&ctl->bar, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  int spins = 0;
+  while (lds_ld(&ctl->bar) < gen) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+      lds_st(&ctl->abort_, 1);
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
+// Gather n granules of `tag` (cooperatively: consumer thread ct of 256 takes pairs ct, ct+256,
+// ...) into the staged-activation planes X (gemv1 layout: element k -> plane (k % EPC) / 4,
+// chunk k / EPC), optionally multiplied by w[k]; returns this thread's sum of squares of the
+// RAW values.  Values in [rs0, rs0 + nres) are also saved to res[].
+template <int EPC>
+__device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, float* X, int KC,
+                                       const float* w, float* res, int rs0, int nres, int ct,
+                                       float& ss, Ctl* ctl, const Clock& clk, int* status) {
+  ss = 0.f;
+  constexpr int B = 8;  // granule pairs in flight per thread
+  for (int base = 2 * ct; base < n; base += 2 * 256 * B) {
+    u32x4v v[B];
+    bool ok[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int i = base + 2 * 256 * j;
+      v[j] = i < n ? gget2(g, i) : u32x4v{0u, tag, 0u, tag};
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) ok[j] = v[j].y == tag && v[j].w == tag;
+    int spins = 0;
+    while (true) {
+      bool all = true;
+#pragma unroll
+      for (int j = 0; j < B; ++j) all &= ok[j];
+      if (all) break;
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        if (!ok[j]) {
+          v[j] = gget2(g, base + 2 * 256 * j);
+          ok[j] = v[j].y == tag && v[j].w == tag;
+        }
+      }
+      if ((++spins & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+        lds_st(&ctl->abort_, 1);
+        __hip_atomic_store(status, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int i = base + 2 * 256 * j;
+      if (i >= n) continue;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int k = i + e;
+        const float x = __uint_as_float(e ? v[j].z : v[j].x);
+        ss = fmaf(x, x, ss);
+        if (k >= rs0 && k < rs0 + nres) res[k - rs0] = x;
+        const float xw = w ? x * w[k] : x;
+        const int m = k / EPC, q = (k % EPC) >> 2;
+        X[(q * KC + m) * 4 + (k & 3)] = xw;
+      }
+    }
+  }
+  return true;
+}
+
+// Dot products of the rows of one ring slot with the staged activation: rows j < nr of
+// rowbytes each (K = rowbytes / esz); lane handles 16-byte chunks m = lane + 64 i.
+template <bool F8, int RPS>
+__device__ __forceinline__ void slot_dot(const uint4* slot, const float4* X, int KC, int nr,
+                                         int lane, float* acc) {
+  constexpr int PL = F8 ? 4 : 2;
+#pragma unroll
+  for (int j = 0; j < RPS; ++j) acc[j] = 0.f;
+  for (int m = lane; m < KC; m += 64) {
+    float4 xq[PL];
+#pragma unroll
+    for (int q = 0; q < PL; ++q) xq[q] = X[q * KC + m];
+#pragma unroll
+    for (int j = 0; j < RPS; ++j) {
+      if (j >= nr) break;
+      const uint4 w = slot[j * KC + m];
+      if (F8) {
+        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
+          const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
+          acc[j] = fmaf(lo.x, xq[q].x, acc[j]);
+          acc[j] = fmaf(lo.y, xq[q].y, acc[j]);
+          acc[j] = fmaf(hi.x, xq[q].z, acc[j]);
+          acc[j] = fmaf(hi.y, xq[q].w, acc[j]);
+        }
+      } else {
+        acc[j] = dot8(w, xq[0], xq[1], acc[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPS; ++j) acc[j] = wave_sum(acc[j]);
+}
+
+__device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, bf16x8& f2) {
+  uint32_t w0[4], w1[4], w2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = x[2 * j], b = x[2 * j + 1];
+    w0[j] = pack2_bf16(a, b);
+    const float a1 = a - bf16_lo(w0[j]), b1 = b - bf16_hi(w0[j]);
+    w1[j] = pack2_bf16(a1, b1);
+    w2[j] = pack2_bf16(a1 - bf16_lo(w1[j]), b1 - bf16_hi(w1[j]));
+  }
+  f0 = __builtin_bit_cast(bf16x8, make_uint4(w0[0], w0[1], w0[2], w0[3]));
+  f1 = __builtin_bit_cast(bf16x8, make_uint4(w1[0], w1[1], w1[2], w1[3]));
+  f2 = __builtin_bit_cast(bf16x8, make_uint4(w2[0], w2[1], w2[2], w2[3]));
+}
+
+// ---------------------------------------------------------------------------------------
+// the kernel
+// ---------------------------------------------------------------------------------------
+template <bool F8, int GRP>
+__global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int NS = a.ring_slots;
+  uint8_t* ring = smem;
+  float* Xa = reinterpret_cast<float*>(smem + (size_t)NS * SLOT);         // H floats
+  float* Xb = Xa + a.H;                                                    // max(F, QD) floats
+  Ctl* ctl = reinterpret_cast<Ctl*>(Xb + a.F);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = gridDim.x, c = blockIdx.x;
+  constexpr int esz = F8 ? 1 : 2;
+  constexpr int EPC = F8 ? 16 : 8;
+  const int H = a.H, QD = a.heads * 128, KVD = a.kv_heads * 128, F = a.F;
+  const int QKVN = QD + 2 * KVD;
+  const int L = a.row_pos[0] + 1;  // attention span of this step (new token at L - 1)
+  const int slot_id = a.row_slot[0];
+  const uint32_t epoch = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Clock clk{__builtin_amdgcn_s_memrealtime() + (uint64_t)a.timeout_ticks};
+
+  if (tid < 8) {
+    ctl->ready[tid] = 0;
+    ctl->freed[tid] = 0;
+  }
+  if (tid == 0) {
+    ctl->bar = 0;
+    ctl->abort_ = 0;
+    ctl->last = 0;
+  }
+  __syncthreads();
+
+  const Ph ph0 = make_ph(a.wqkv, QKVN, H, esz, G, c, true), ph1 = make_ph(a.wo, H, QD, esz, G, c, false),
+           ph2 = make_ph(a.wgu, 2 * F, H, esz, G, c, true), ph3 = make_ph(a.wd, H, F, esz, G, c, false);
+
+  if (wid == 0) {
+    // ================================ LOADER ================================
+    int k = 0, pend_lo = 0;  // slots [pend_lo, k) issued, not yet published
+    int ips1 = 0, ips2 = 0;  // instructions of the newest two issued slots (k - 1, k - 2)
+    int spins = 0;
+    bool dead = false;
+    auto publish_all = [&]() {
+      wait_vm<0>();
+      for (int q = pend_lo; q < k; ++q) lds_st(&ctl->ready[q % NS], q + 1);
+      pend_lo = k;
+    };
+    auto stream_phase = [&](const Ph& P, int l) {
+      const uint8_t* Wl = P.W + (size_t)l * P.layer_bytes;
+      const size_t lim = P.layer_bytes - 16;
+      for (int s = 0; s < P.nslots; ++s) {
+        const int pos = k % NS;
+        if (k >= NS && lds_ld(&ctl->freed[pos]) != k - NS + 1) {
+          publish_all();
+          while (lds_ld(&ctl->freed[pos]) != k - NS + 1) {
+            __builtin_amdgcn_s_sleep(2);
+            if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+              dead = true;
+              return;
+            }
+          }
+        }
+        const size_t off0 = (size_t)(P.r0 + s * P.rps) * P.rowbytes + (size_t)lane * 16;
+        uint8_t* dst = ring + (size_t)pos * SLOT;
+        for (int i = 0; i < P.ips; ++i) {
+          const size_t off = min(off0 + (size_t)i * 1024, lim);
+          __builtin_amdgcn_global_load_lds((gbl_cvoid*)(Wl + off), (lds_void*)(dst + i * 1024), 16, 0, 2);
+        }
+        ips2 = ips1;
+        ips1 = P.ips;
+        ++k;
+        if (k - pend_lo > DEPTH) {  // the oldest pending slot has landed once only the DEPTH newer remain
+          wait_vm_n(ips1 + ips2);
+          lds_st(&ctl->ready[pend_lo % NS], pend_lo + 1);
+          ++pend_lo;
+        }
+      }
+    };
+    for (int l = 0; l < a.layers && !dead; ++l) {
+      stream_phase(ph0, l);
+      if (!dead) stream_phase(ph1, l);
+      if (!dead) stream_phase(ph2, l);
+      if (!dead) stream_phase(ph3, l);
+    }
+    publish_all();
+    if (dead) lds_st(&ctl->abort_, 1);
+  } else {
+    // =============================== CONSUMERS ===============================
+    const int cw = wid - 1, ct = tid - 64;
+    int gen = 0;
+    bool ok = true;
+    int k = 0;  // global slot index, same walk as the loader
+    const float4* Xa4 = reinterpret_cast<const float4*>(Xa);
+    const float4* Xb4 = reinterpret_cast<const float4*>(Xb);
+    const int KC_H = H / EPC, KC_Q = QD / EPC, KC_F = F / EPC;
+    // attention items: S splits x kv heads, item i on CU i * G / items
+    const int S = (L + SL - 1) / SL;
+    const int items = S * a.kv_heads;
+    const float att_scale = 1.0f / sqrtf(128.0f);
+
+    // wait for ring slot k; returns its LDS base (nullptr on abort)
+    auto take = [&](int kk) -> const uint4* {
+      const int pos = kk % NS;
+      int spins = 0;
+      while (lds_ld(&ctl->ready[pos]) != kk + 1) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+          lds_st(&ctl->abort_, 1);
+          if (lane == 0) __hip_atomic_store(a.status, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return nullptr;
+        }
+      }
+      return reinterpret_cast<const uint4*>(ring + (size_t)pos * SLOT);
+    };
+    auto give = [&](int kk) { lds_st(&ctl->freed[kk % NS], kk + 1); };
+
+    for (int l = 0; l < a.layers && ok; ++l) {
+      const uint32_t tg = (epoch << 8) | ((uint32_t)l << 3);
+      uint16_t* kc = a.kcache + a.kv_layer_elems * l;
+      uint16_t* vc = a.vcache + a.kv_layer_elems * l;
+      // ---------------- QKV ----------------
+      {
+        float ss = 0.f;
+        const float* nw = a.attn_norm + (size_t)l * H;
+        if (l == 0) {  // the decode row's hidden state (previous launch: plain loads)
+          for (int kk = ct; kk < H; kk += 256) {
+            const float x = a.h[kk];
+            ss = fmaf(x, x, ss);
+            if (kk >= ph1.r0 && kk < ph1.r1) ctl->res1[kk - ph1.r0] = x;
+            Xa[((((kk % EPC) >> 2) * KC_H) + kk / EPC) * 4 + (kk & 3)] = x * nw[kk];
+          }
+        } else {
+          ok = gather<EPC>(a.g_h2, H, tg - 8 + PH_H2, Xa, KC_H, nw, ctl->res1, ph1.r0,
+                           ph1.r1 - ph1.r0, ct, ss, ctl, clk, a.status);
+          if (!ok) break;
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) ctl->ss[cw] = ss;
+        if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+        const float scale = 1.0f / sqrtf((ctl->ss[0] + ctl->ss[1] + ctl->ss[2] + ctl->ss[3]) / H + a.eps);
+        const Ph& P = ph0;
+        const int pos = L - 1;
+        for (int s = 0; s < P.nslots; ++s, ++k) {
+          if (k % NC != cw) continue;
+          const uint4* sl = take(k);
+          if (!sl) { ok = false; break; }
+          const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
+          float acc[4];
+          slot_dot<F8, F8 ? 4 : 2>(sl, Xa4, KC_H, nr, lane, acc);
+          give(k);
+          if (lane == 0) {
+            for (int j = 0; j + 1 < nr; j += 2) {
+              const int n = n0 + j;
+              float x1 = acc[j] * scale, x2 = acc[j + 1] * scale;
+              if (F8) {
+                x1 *= a.sqkv[(size_t)l * QKVN + n];
+                x2 *= a.sqkv[(size_t)l * QKVN + n + 1];
+              }
+              const int hh = n >> 7, within = n & 127, p = within >> 1;
+              if (hh < a.heads + a.kv_heads) {
+                const float cs = a.rope_cos[(size_t)pos * 64 + p], sn = a.rope_sin[(size_t)pos * 64 + p];
+                const float o1 = x1 * cs - x2 * sn, o2 = x2 * cs + x1 * sn;
+                if (hh < a.heads) {
+                  gput(a.g_qkv, hh * 128 + p, o1, tg + PH_QKV);
+                  gput(a.g_qkv, hh * 128 + p + 64, o2, tg + PH_QKV);
+                } else {
+                  const int kh = hh - a.heads;
+                  const uint16_t b1 = f32_to_bf16(o1), b2 = f32_to_bf16(o2);
+                  uint16_t* kk2 = kc + ((size_t)slot_id * a.kv_heads + kh) * a.max_pos * 128;
+                  kk2[kv_k_off(pos, p)] = b1;
+                  kk2[kv_k_off(pos, p + 64)] = b2;
+                  gput(a.g_qkv, QD + kh * 128 + p, bf16_to_f32(b1), tg + PH_QKV);
+                  gput(a.g_qkv, QD + kh * 128 + p + 64, bf16_to_f32(b2), tg + PH_QKV);
+                }
+              } else {
+                const int vh = hh - a.heads - a.kv_heads;
+                const uint16_t b1 = f32_to_bf16(x1), b2 = f32_to_bf16(x2);
+                uint16_t* vv = vc + ((size_t)slot_id * a.kv_heads + vh) * 128 * a.max_pos;
+                vv[kv_v_off(pos, within)] = b1;
+                vv[kv_v_off(pos, within + 1)] = b2;
+                gput(a.g_qkv, QD + KVD + vh * 128 + within, bf16_to_f32(b1), tg + PH_QKV);
+                gput(a.g_qkv, QD + KVD + vh * 128 + within + 1, bf16_to_f32(b2), tg + PH_QKV);
+              }
+            }
+          }
+        }
+        if (!ok) break;
+      }
+      // ---------------- ATTENTION ----------------
+      for (int it = 0; it < items; ++it) {
+        // item it = (kv head, split) runs on CU it * G / items (spread over the grid)
+        if (it * G / items != c) continue;
+        const int kvh = it % a.kv_heads, sp = it / a.kv_heads;
+        const int p0 = sp * SL, p1 = min(p0 + SL, L);  // positions [p0, p1) of this split
+        const bool has_new = p1 == L;                  // holds position L - 1 (granules)
+        const int Lc = L - 1;                          // cached positions
+        // scratch in Xb: q [GRP][128], k/v of the new position, wave partials
+        float* qs = Xb;
+        float* kn = qs + GRP * 128;
+        float* vn = kn + 128;
+        float* wacc = vn + 128;                        // [NC + 1][GRP][128]
+        float* wml = wacc + (NC + 1) * GRP * 128;      // [NC + 1][GRP][2]
+        const size_t head = (size_t)slot_id * a.kv_heads + kvh;
+        const uint4* Kf = reinterpret_cast<const uint4*>(kc) + head * a.max_pos * 16;
+        const uint4* Vf = reinterpret_cast<const uint4*>(vc) + head * a.max_pos * 16;
+        const int base = p0 + 32 * cw;                 // this wave's chunk
+        const bool live = base < min(p1, Lc);
+        uint4 kf[2][4], vf[8];
+        if (live) {  // cached K / V chunk loads go out before the q wait
+          const uint4* kcp = Kf + (size_t)(base >> 5) * 512 + lane;
+          const uint4* vcp = Vf + (size_t)(base >> 5) * 512 + lane;
+#pragma unroll
+          for (int T = 0; T < 2; ++T)
+#pragma unroll
+            for (int st = 0; st < 4; ++st) kf[T][st] = kcp[(T * 4 + st) * 64];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) vf[t] = vcp[t * 64];
+        }
+        // gather q (GRP heads) and, for the last split, the new k / v
+        {
+          float dummy;
+          ok = gather<4>(a.g_qkv + (size_t)kvh * GRP * 128, GRP * 128, tg + PH_QKV, qs, GRP * 32,
+                         nullptr, nullptr, 0, 0, ct, dummy, ctl, clk, a.status);
+          // (EPC 4: plane 0 only, i.e. qs[k] in natural order)
+          if (ok && has_new) {
+            ok = gather<4>(a.g_qkv + QD + kvh * 128, 128, tg + PH_QKV, kn, 32, nullptr, nullptr, 0, 0,
+                           ct, dummy, ctl, clk, a.status);
+            if (ok)
+              ok = gather<4>(a.g_qkv + QD + KVD + kvh * 128, 128, tg + PH_QKV, vn, 32, nullptr, nullptr,
+                             0, 0, ct, dummy, ctl, clk, a.status);
+          }
+          if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
+        }
+        const int cc = lane & 15, g = lane >> 4;
+        float M = -INFINITY, lsum = 0.f;
+        f32x4 acc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (live) {
+          bf16x8 qf[3][4];
+          {
+            const int hq = cc < GRP ? cc : 0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+              float x[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) x[j] = cc < GRP ? qs[hq * 128 + 32 * st + 8 * g + j] : 0.f;
+              split3(x, qf[0][st], qf[1][st], qf[2][st]);
+            }
+          }
+          f32x4 sc[2];
+#pragma unroll
+          for (int T = 0; T < 2; ++T) {
+            sc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+              const bf16x8 kb = __builtin_bit_cast(bf16x8, kf[T][st]);
+#pragma unroll
+              for (int pt = 0; pt < 3; ++pt)
+                sc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb, qf[pt][st], sc[T], 0, 0, 0);
+            }
+          }
+          const int lim = min(p1, Lc);
+          float sv[8], mc = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int p = base + 8 * g + j;
+            sv[j] = p < lim ? sc[j >> 2][j & 3] * att_scale : -INFINITY;
+            mc = fmaxf(mc, sv[j]);
+          }
+          mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+          mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+          M = mc;
+          float pv[8], ps = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pv[j] = expf(sv[j] - M);
+            ps += pv[j];
+          }
+          ps += __shfl_xor(ps, 16, 64);
+          ps += __shfl_xor(ps, 32, 64);
+          lsum = ps;
+          bf16x8 pf[3];
+          split3(pv, pf[0], pf[1], pf[2]);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const bf16x8 vb = __builtin_bit_cast(bf16x8, vf[t]);
+#pragma unroll
+            for (int pt = 0; pt < 3; ++pt)
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt], vb, acc[t], 0, 0, 0);
+          }
+        }
+        // wave partial -> LDS (head c's (M, l) in lanes c; O rows: lane (c, g = 0) holds heads i)
+        if (g == 0 && cc < GRP) {
+          wml[(cw * GRP + cc) * 2] = M;
+          wml[(cw * GRP + cc) * 2 + 1] = lsum;
+        }
+        if (g == 0) {
+#pragma unroll
+          for (int i = 0; i < GRP; ++i)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) wacc[(cw * GRP + i) * 128 + 16 * t + cc] = acc[t][i];
+        }
+        // the new position: one more "wave" partial per head (score, 1, v)
+        if (has_new && cw == 0 && lane < GRP) {
+          float sdot = 0.f;
+          for (int d = 0; d < 128; ++d) sdot = fmaf(qs[lane * 128 + d], kn[d], sdot);
+          wml[(NC * GRP + lane) * 2] = sdot * att_scale;
+          wml[(NC * GRP + lane) * 2 + 1] = 1.f;
+        }
+        if (has_new && cw == 1) {
+          for (int i = lane; i < GRP * 128; i += 64) wacc[NC * GRP * 128 + i] = vn[i & 127];
+        }
+        if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+        // merge the NC (+1) wave partials: consumer thread ct -> outputs idx = ct, ct + 256, ...
+        const int nparts = has_new ? NC + 1 : NC;
+        float* part = a.part + (size_t)kvh * a.smax * GRP * 130;
+        const bool single = S == 1;
+        for (int idx = ct; idx < GRP * 128; idx += 256) {
+          const int h = idx >> 7, td = idx & 127;
+          float Mb = -INFINITY;
+          for (int w = 0; w < nparts; ++w) Mb = fmaxf(Mb, wml[(w * GRP + h) * 2]);
+          float num = 0.f, den = 0.f;
+          for (int w = 0; w < nparts; ++w) {
+            const float mw = wml[(w * GRP + h) * 2];
+            const float f = mw == -INFINITY ? 0.f : expf(mw - Mb);
+            num = fmaf(f, wacc[(w * GRP + h) * 128 + td], num);
+            den = fmaf(f, wml[(w * GRP + h) * 2 + 1], den);
+          }
+          if (single) {
+            gput(a.g_att, (kvh * GRP + h) * 128 + td, num / den, tg + PH_ATT);
+          } else {
+            float* pp = part + ((size_t)sp * GRP + h) * 130;
+            st_wt(pp + td, num);
+            if (td == 0) {
+              st_wt(pp + 128, Mb);
+              st_wt(pp + 129, den);
+            }
+          }
+        }
+        if (!single) {
+          if (!(ok = cbar(ctl, gen, clk, a.status))) break;  // (cbar waits vmcnt(0): partials landed)
+          if (ct == 0) {
+            int* tk = a.tickets + l * a.kv_heads + kvh;
+            const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == S - 1;
+            if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds_st(&ctl->last, last);
+          }
+          if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+          if (lds_ld(&ctl->last)) {  // the last split of this kv head merges all S
+            for (int idx = ct; idx < GRP * 128; idx += 256) {
+              const int h = idx >> 7, td = idx & 127;
+              float Mb = -INFINITY;
+              for (int s2 = 0; s2 < S; ++s2) Mb = fmaxf(Mb, ld_wt(part + ((size_t)s2 * GRP + h) * 130 + 128));
+              float num = 0.f, den = 0.f;
+              for (int s2 = 0; s2 < S; ++s2) {
+                const float* pp = part + ((size_t)s2 * GRP + h) * 130;
+                const float mw = ld_wt(pp + 128);
+                const float f = mw == -INFINITY ? 0.f : expf(mw - Mb);
+                num = fmaf(f, ld_wt(pp + td), num);
+                den = fmaf(f, ld_wt(pp + 129), den);
+              }
+              gput(a.g_att, (kvh * GRP + h) * 128 + td, num / den, tg + PH_ATT);
+            }
+          }
+        }
+        if (!(ok = cbar(ctl, gen, clk, a.status))) break;  // scratch reused by the next item
+      }
+      if (!ok) break;
+      // ---------------- O-PROJ ----------------
+      {
+        float ss;
+        ok = gather<EPC>(a.g_att, QD, tg + PH_ATT, Xb, KC_Q, nullptr, nullptr, 0, 0, ct, ss, ctl,
+                         clk, a.status);
+        if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
+        const Ph& P = ph1;
+        for (int s = 0; s < P.nslots; ++s, ++k) {
+          if (k % NC != cw) continue;
+          const uint4* sl = take(k);
+          if (!sl) { ok = false; break; }
+          const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
+          float acc[4];
+          slot_dot<F8, F8 ? 4 : 2>(sl, Xb4, KC_Q, nr, lane, acc);
+          give(k);
+          if (lane < nr) {
+            float y = acc[0];
+#pragma unroll
+            for (int j = 1; j < 4; ++j) y = lane == j ? acc[j] : y;
+            const int n = n0 + lane;
+            if (F8) y *= a.so[(size_t)l * H + n];
+            gput(a.g_h1, n, ctl->res1[n - P.r0] + y, tg + PH_H1);
+          }
+        }
+        if (!ok) break;
+      }
+      // ---------------- GATE / UP ----------------
+      {
+        float ss;
+        ok = gather<EPC>(a.g_h1, H, tg + PH_H1, Xa, KC_H, a.mlp_norm + (size_t)l * H, ctl->res2,
+                         ph3.r0, ph3.r1 - ph3.r0, ct, ss, ctl, clk, a.status);
+        if (!ok) break;
+        ss = wave_sum(ss);
+        if (lane == 0) ctl->ss[cw] = ss;
+        if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+        const float scale = 1.0f / sqrtf((ctl->ss[0] + ctl->ss[1] + ctl->ss[2] + ctl->ss[3]) / H + a.eps);
+        const Ph& P = ph2;
+        for (int s = 0; s < P.nslots; ++s, ++k) {
+          if (k % NC != cw) continue;
+          const uint4* sl = take(k);
+          if (!sl) { ok = false; break; }
+          const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
+          float acc[4];
+          slot_dot<F8, F8 ? 4 : 2>(sl, Xa4, KC_H, nr, lane, acc);
+          give(k);
+          // pair j (rows n0 + 2j, n0 + 2j + 1) -> lane j
+          if (2 * lane + 1 < nr) {
+            float gt = acc[0] * scale, up = acc[1] * scale;
+            if (lane == 1) { gt = acc[2] * scale; up = acc[3] * scale; }
+            const int n = n0 + 2 * lane;
+            if (F8) {
+              gt *= a.sgu[(size_t)l * 2 * F + n];
+              up *= a.sgu[(size_t)l * 2 * F + n + 1];
+            }
+            gput(a.g_act, n >> 1, gt / (1.0f + expf(-gt)) * up, tg + PH_ACT);
+          }
+        }
+        if (!ok) break;
+      }
+      // ---------------- DOWN ----------------
+      {
+        float ss;
+        ok = gather<EPC>(a.g_act, F, tg + PH_ACT, Xb, KC_F, nullptr, nullptr, 0, 0, ct, ss, ctl, clk,
+                         a.status);
+        if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
+        const Ph& P = ph3;
+        const bool last_layer = l == a.layers - 1;
+        for (int s = 0; s < P.nslots; ++s, ++k) {
+          if (k % NC != cw) continue;
+          const uint4* sl = take(k);
+          if (!sl) { ok = false; break; }
+          const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
+          float acc[2];
+          slot_dot<F8, F8 ? 2 : 1>(sl, Xb4, KC_F, nr, lane, acc);
+          give(k);
+          if (lane < nr) {
+            float y = lane == 0 ? acc[0] : acc[F8 ? 1 : 0];
+            const int n = n0 + lane;
+            if (F8) y *= a.sd[(size_t)l * H + n];
+            const float v = ctl->res2[n - P.r0] + y;
+            if (last_layer) a.h[n] = v;
+            else gput(a.g_h2, n, v, tg + PH_H2);
+          }
+        }
+        if (!ok) break;
+      }
+    }
+    if (!ok) lds_st(&ctl->abort_, 1);
+  }
+  __syncthreads();
+  // the last workgroup to finish advances the epoch (every workgroup read it at entry: none
+  // can finish before all have started, since every phase needs every CU's outputs)
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(a.epoch + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (unsigned)G - 1) {
+      __hip_atomic_store(a.epoch + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t e = epoch + 1;
+      if ((e & 0xffffffu) == 0) e += 1;  // tag 0 is never a valid epoch (zeroed buffers)
+      __hip_atomic_store(a.epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace eng
+
+size_t engine_lds_bytes(int ring_slots, int H, int F) {
+  return (size_t)ring_slots * eng::SLOT + (size_t)(H + F) * 4 + sizeof(eng::Ctl);
+}
+
+// Workgroups of the engine one CU holds at once (it needs exactly one per CU, all co-resident)
+hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
+  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+  const int grp = a.heads / a.kv_heads;
+  const void* fn = nullptr;
+#define MX_ENGF(F8_, G_) if (a.f8 == F8_ && grp == G_) fn = reinterpret_cast<const void*>(&eng::engine_kernel<F8_, G_>);
+  MX_ENGF(false, 3) MX_ENGF(true, 3) MX_ENGF(false, 2) MX_ENGF(true, 2)
+  MX_ENGF(false, 4) MX_ENGF(true, 4) MX_ENGF(false, 1) MX_ENGF(true, 1)
+#undef MX_ENGF
+  if (!fn) return hipErrorNotSupported;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, eng::NT, lds);
+}
+
+hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
+  const int grp = a.heads / a.kv_heads;
+  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+  if (a.ring_slots < 3 || a.ring_slots > 8 || lds > 160 * 1024 || a.layers > 31) return hipErrorInvalidValue;
+  if (a.H % 1024 || a.F % 1024 || a.heads * 128 != a.H || grp < 1 || grp > 4) return hipErrorNotSupported;
+#define MX_ENG(F8_, G_)                                                                       \
+  if (a.f8 == F8_ && grp == G_) {                                                             \
+    hipLaunchKernelGGL((eng::engine_kernel<F8_, G_>), dim3(grid), dim3(eng::NT), lds, st, a);  \
+    return hipGetLastError();                                                                  \
+  }
+  MX_ENG(false, 3) MX_ENG(true, 3) MX_ENG(false, 2) MX_ENG(true, 2)
+  MX_ENG(false, 4) MX_ENG(true, 4) MX_ENG(false, 1) MX_ENG(true, 1)
+#undef MX_ENG
+  return hipErrorNotSupported;
+}
+
+}  // namespace mx

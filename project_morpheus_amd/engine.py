@@ -96,7 +96,8 @@ class LlmEngine:
         """One step for rows [0, n_rows), each under its slot's generation parameters."""
         self._check(self.lib.mx_llm_decode(self.h, n_rows, C.c_void_p(stream.cuda_stream)))
 
-    PROFILE_CLASSES = ("qkv", "attention", "o_proj", "gate_up", "down", "lm_head", "commit")
+    PROFILE_CLASSES = ("qkv", "attention", "o_proj", "gate_up", "down", "lm_head", "commit",
+                       "engine")
 
     def decode_profiled(self, n_rows: int, stream) -> Dict[str, float]:
         """One eager step with HIP events around every launch: ms per launch class

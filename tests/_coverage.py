@@ -92,6 +92,13 @@ GPU_RUNS = {
         [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, f8=True)],
     "test_gpu_fp8.py::test_fp8_rows_merge_straddling_splits_orpheus_width[nsm4]":
         [_r(ORPHEUS_16K, [200, 260, 330, 480, 520, 600, 700, 760], 12, f8=True)],
+    # ---- the persistent one-row engine (option b1_engine) ----------------------------
+    "test_gpu_engine_b1.py::test_engine_orpheus_width[bf16]":
+        [_r(ORPHEUS_16K, [600], 40, b1_engine=1)],
+    "test_gpu_engine_b1.py::test_engine_orpheus_width[fp8]":
+        [_r(ORPHEUS_16K, [600], 40, f8=True, b1_engine=1)],
+    "test_gpu_engine_b1.py::test_engine_full_depth_orpheus_3b":
+        [_r(ORPHEUS, [30], 10, b1_engine=1)],
     # ---- sampling -------------------------------------------------------------------
     "test_gpu_sampling.py::test_sampling_one_row_hidden_3072_product_mode":
         [_r(ORPHEUS_16K, [9], 12)] * 3,

@@ -46,7 +46,7 @@ FP8_SMALL = Dims(1024, 8, 2, 2048, 1000)
 DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
                 rows_nt_max=0, rows_head_target=0, rows_head_mt=2, head_b1=1, rpw_o=0,
-                rpw_gu=0, rpw_down=0, legacy_gemv=0)
+                rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7)
 
 
 def _b(v):
@@ -204,6 +204,10 @@ def forward_keys(d, R, max_len, f8, opts=None, head_rows=None, sample=False):
     o = dict(DEFAULTS, **(opts or {}))
     H, QD = d.hidden, d.heads * 128
     keys = set()
+    if R == 1 and head_rows is None and o["b1_engine"]:  # capi.hip enqueue_decode
+        keys.add(f"eng::engine_kernel<{_b(f8)}, {d.grp}>")
+        keys.add(gemv_launch(d.vocab, H, 1, EPI_ARGMAX, True, f8, o))
+        return keys
     keys.add(gemv_launch(QD + 2 * d.kv_heads * 128, H, R, EPI_QKV, True, f8, o))
     nw, cpw, nsplit = att_shape(d, R, max_len, o)
     keys.add(f"attn_kernel<{d.grp}, {cpw}, {nw}>" + (PREFILL_TAG if head_rows == 1 and R > 1 else ""))
