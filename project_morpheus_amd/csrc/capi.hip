@@ -1106,8 +1106,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
       MX_TRY(x, hipSetDevice(x->device));
       int cus = 0, per_cu = 0;
       MX_TRY(x, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, x->device));
+      // per-CU row counts must fit the engine's LDS tables (engine_b1.hip Ctl: 32 qkv / o /
+      // down rows, 64 gate/up rows)
+      auto per = [&](int n) { return (((n + cus - 1) / cus) + 1) & ~1; };
+      const int qkv_rows = (c.heads + 2 * c.kv_heads) * 128;
       if (c.hidden % 1024 || c.ffn % 1024 || c.heads * 128 != c.hidden || c.layers > 31 ||
-          c.heads / c.kv_heads > 4 || (c.hidden + cus - 1) / cus > 32)
+          c.heads / c.kv_heads > 4 || per(c.hidden) > 32 || per(qkv_rows) > 32 || per(2 * c.ffn) > 64)
         MX_FAIL(x, MX_ERR_ARG, "b1_engine: model shape outside the engine's (hidden = heads x 128, "
                                "multiples of 1024, <= 31 layers, GQA <= 4)");
       EngineArgs ea = engine_args(x);

@@ -90,7 +90,11 @@ struct Ctl {           // LDS control block
   int pad;
   float ss[NC];        // per-wave partial sums of squares
   float res1[32], res2[32];  // this CU's residual slice (o-proj / down rows)
+  float rope[32][2];   // cos / sin at the step's position for this CU's qkv row pairs
+  float scl[2][160];   // e4m3 row scales of this CU's rows, by layer parity:
+                       // [0, 32) qkv, [32, 64) o, [64, 128) gate/up, [128, 160) down
 };
+constexpr int SC_QKV = 0, SC_O = 32, SC_GU = 64, SC_D = 128;
 
 struct Clock {
   uint64_t deadline;
@@ -118,7 +122,7 @@ __device__ __forceinline__ Ph make_ph(const void* W, int N, int K, int esz, int 
   if (pair) per = (per + 1) & ~1;
   p.r0 = min(N, c * per);
   p.r1 = min(N, p.r0 + per);
-  p.rps = SLOT / p.rowbytes;
+  p.rps = min(SLOT / p.rowbytes, 4);  // (the consumers' slot_dot handles up to 4 rows)
   if (pair) p.rps &= ~1;
   p.ips = p.rps * p.rowbytes / 1024;
   p.nslots = (p.r1 - p.r0 + p.rps - 1) / p.rps;
@@ -168,14 +172,17 @@ __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, floa
                                        const float* w, float* res, int rs0, int nres, int ct,
                                        float& ss, Ctl* ctl, const Clock& clk, int* status) {
   ss = 0.f;
-  constexpr int B = 8;  // granule pairs in flight per thread
+  constexpr int B = 8;  // granule pairs in flight per thread (n <= 4096 in one round)
   for (int base = 2 * ct; base < n; base += 2 * 256 * B) {
     u32x4v v[B];
     bool ok[B];
+    float2 wv[B];
 #pragma unroll
     for (int j = 0; j < B; ++j) {
       const int i = base + 2 * 256 * j;
       v[j] = i < n ? gget2(g, i) : u32x4v{0u, tag, 0u, tag};
+      // the norm weights go out with the granules (not after the wait)
+      wv[j] = (w && i < n) ? *reinterpret_cast<const float2*>(w + i) : make_float2(1.f, 1.f);
     }
 #pragma unroll
     for (int j = 0; j < B; ++j) ok[j] = v[j].y == tag && v[j].w == tag;
@@ -209,7 +216,7 @@ __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, floa
         const float x = __uint_as_float(e ? v[j].z : v[j].x);
         ss = fmaf(x, x, ss);
         if (k >= rs0 && k < rs0 + nres) res[k - rs0] = x;
-        const float xw = w ? x * w[k] : x;
+        const float xw = x * (e ? wv[j].y : wv[j].x);
         const int m = k / EPC, q = (k % EPC) >> 2;
         X[(q * KC + m) * 4 + (k & 3)] = xw;
       }
@@ -391,6 +398,29 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       uint16_t* vc = a.vcache + a.kv_layer_elems * l;
       // ---------------- QKV ----------------
       {
+        // this layer's e4m3 row scales and (once) the rope factors of the step's position, to
+        // LDS: read in the slot epilogues, visible after the gather's barrier below (the
+        // scales are double-buffered by layer parity: a wave may still be in the previous
+        // layer's down-projection epilogue)
+        if (l == 0) {
+          for (int j = ct; 2 * j < ph0.r1 - ph0.r0; j += 256) {
+            const int p = ((ph0.r0 + 2 * j) & 127) >> 1;
+            ctl->rope[j][0] = a.rope_cos[(size_t)(L - 1) * 64 + p];
+            ctl->rope[j][1] = a.rope_sin[(size_t)(L - 1) * 64 + p];
+          }
+        }
+        if (F8) {
+          float* sc = ctl->scl[l & 1];
+          for (int j = ct; j < 160; j += 256) {
+            const float* src = nullptr;
+            int r = 0;
+            if (j < SC_O) { r = ph0.r0 + j; src = r < ph0.r1 ? a.sqkv + (size_t)l * QKVN + r : nullptr; }
+            else if (j < SC_GU) { r = ph1.r0 + j - SC_O; src = r < ph1.r1 ? a.so + (size_t)l * H + r : nullptr; }
+            else if (j < SC_D) { r = ph2.r0 + j - SC_GU; src = r < ph2.r1 ? a.sgu + (size_t)l * 2 * F + r : nullptr; }
+            else { r = ph3.r0 + j - SC_D; src = r < ph3.r1 ? a.sd + (size_t)l * H + r : nullptr; }
+            sc[j] = src ? *src : 0.f;
+          }
+        }
         float ss = 0.f;
         const float* nw = a.attn_norm + (size_t)l * H;
         if (l == 0) {  // the decode row's hidden state (previous launch: plain loads)
@@ -424,12 +454,12 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
               const int n = n0 + j;
               float x1 = acc[j] * scale, x2 = acc[j + 1] * scale;
               if (F8) {
-                x1 *= a.sqkv[(size_t)l * QKVN + n];
-                x2 *= a.sqkv[(size_t)l * QKVN + n + 1];
+                x1 *= ctl->scl[l & 1][SC_QKV + n - P.r0];
+                x2 *= ctl->scl[l & 1][SC_QKV + n + 1 - P.r0];
               }
               const int hh = n >> 7, within = n & 127, p = within >> 1;
               if (hh < a.heads + a.kv_heads) {
-                const float cs = a.rope_cos[(size_t)pos * 64 + p], sn = a.rope_sin[(size_t)pos * 64 + p];
+                const float cs = ctl->rope[(n - P.r0) >> 1][0], sn = ctl->rope[(n - P.r0) >> 1][1];
                 const float o1 = x1 * cs - x2 * sn, o2 = x2 * cs + x1 * sn;
                 if (hh < a.heads) {
                   gput(a.g_qkv, hh * 128 + p, o1, tg + PH_QKV);
@@ -620,17 +650,37 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           }
           if (!(ok = cbar(ctl, gen, clk, a.status))) break;
           if (lds_ld(&ctl->last)) {  // the last split of this kv head merges all S
+            // MC splits' (m, l, acc) loads in flight per round (one round up to L = 1,024),
+            // merged online in split order
+            constexpr int MC = 8;
             for (int idx = ct; idx < GRP * 128; idx += 256) {
               const int h = idx >> 7, td = idx & 127;
-              float Mb = -INFINITY;
-              for (int s2 = 0; s2 < S; ++s2) Mb = fmaxf(Mb, ld_wt(part + ((size_t)s2 * GRP + h) * 130 + 128));
-              float num = 0.f, den = 0.f;
-              for (int s2 = 0; s2 < S; ++s2) {
-                const float* pp = part + ((size_t)s2 * GRP + h) * 130;
-                const float mw = ld_wt(pp + 128);
-                const float f = mw == -INFINITY ? 0.f : expf(mw - Mb);
-                num = fmaf(f, ld_wt(pp + td), num);
-                den = fmaf(f, ld_wt(pp + 129), den);
+              float Mb = -INFINITY, num = 0.f, den = 0.f;
+              for (int s0 = 0; s0 < S; s0 += MC) {
+                float mv[MC], lv[MC], av[MC];
+#pragma unroll
+                for (int j = 0; j < MC; ++j) {
+                  const float* pp = part + ((size_t)min(s0 + j, S - 1) * GRP + h) * 130;
+                  mv[j] = ld_wt(pp + 128);
+                  lv[j] = ld_wt(pp + 129);
+                  av[j] = ld_wt(pp + td);
+                }
+                float mn = Mb;
+#pragma unroll
+                for (int j = 0; j < MC; ++j)
+                  if (s0 + j < S) mn = fmaxf(mn, mv[j]);
+                const float r = Mb == -INFINITY ? 0.f : expf(Mb - mn);
+                num *= r;
+                den *= r;
+#pragma unroll
+                for (int j = 0; j < MC; ++j) {
+                  if (s0 + j < S) {
+                    const float f = mv[j] == -INFINITY ? 0.f : expf(mv[j] - mn);
+                    num = fmaf(f, av[j], num);
+                    den = fmaf(f, lv[j], den);
+                  }
+                }
+                Mb = mn;
               }
               gput(a.g_att, (kvh * GRP + h) * 128 + td, num / den, tg + PH_ATT);
             }
@@ -659,7 +709,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
 #pragma unroll
             for (int j = 1; j < 4; ++j) y = lane == j ? acc[j] : y;
             const int n = n0 + lane;
-            if (F8) y *= a.so[(size_t)l * H + n];
+            if (F8) y *= ctl->scl[l & 1][SC_O + n - P.r0];
             gput(a.g_h1, n, ctl->res1[n - P.r0] + y, tg + PH_H1);
           }
         }
@@ -690,8 +740,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
             if (lane == 1) { gt = acc[2] * scale; up = acc[3] * scale; }
             const int n = n0 + 2 * lane;
             if (F8) {
-              gt *= a.sgu[(size_t)l * 2 * F + n];
-              up *= a.sgu[(size_t)l * 2 * F + n + 1];
+              gt *= ctl->scl[l & 1][SC_GU + n - P.r0];
+              up *= ctl->scl[l & 1][SC_GU + n + 1 - P.r0];
             }
             gput(a.g_act, n >> 1, gt / (1.0f + expf(-gt)) * up, tg + PH_ACT);
           }
@@ -717,7 +767,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (lane < nr) {
             float y = lane == 0 ? acc[0] : acc[F8 ? 1 : 0];
             const int n = n0 + lane;
-            if (F8) y *= a.sd[(size_t)l * H + n];
+            if (F8) y *= ctl->scl[l & 1][SC_D + n - P.r0];
             const float v = ctl->res2[n - P.r0] + y;
             if (last_layer) a.h[n] = v;
             else gput(a.g_h2, n, v, tg + PH_H2);
