@@ -106,7 +106,8 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
- * launch, engine_b1.hip), "engine_slots" (its LDS ring depth, set before b1_engine).  Drops
+ * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
+ * flight, 2 or 3).  Drops
  * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
 /* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,

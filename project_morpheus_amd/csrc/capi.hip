@@ -144,7 +144,7 @@ struct mx_llm {
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent one-row engine (engine_b1.hip): option b1_engine runs the layers of a
   // one-row decode step as one launch (engine_slots = its LDS ring depth)
-  int b1_engine = 0, engine_slots = 7, engine_grid = 0;
+  int b1_engine = 0, engine_slots = 7, engine_depth = 2, engine_grid = 0;
   uint2 *g_qkv = nullptr, *g_att = nullptr, *g_h1 = nullptr, *g_act = nullptr, *g_h2 = nullptr;
   float* eng_part = nullptr;
   int* eng_tickets = nullptr;
@@ -777,7 +777,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.part = x->eng_part; a.tickets = x->eng_tickets; a.epoch = x->eng_epoch; a.status = x->eng_status_d;
   a.layers = c.layers; a.H = c.hidden; a.heads = c.heads; a.kv_heads = c.kv_heads; a.F = c.ffn;
   a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
-  a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps;
+  a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth;
   a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
   return a;
 }
@@ -1095,12 +1095,15 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_mt") {
     if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_head_mt must be 1 or 2");
     x->rows_head_mt = value;
-  } else if (k == "b1_engine" || k == "engine_slots") {
+  } else if (k == "b1_engine" || k == "engine_slots" || k == "engine_depth") {
     const bool en = k == "b1_engine" ? value != 0 : x->b1_engine != 0;
     const int slots = k == "engine_slots" ? value : x->engine_slots;
+    const int depth = k == "engine_depth" ? value : x->engine_depth;
     if (k == "b1_engine" && value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine must be 0 or 1");
-    if (slots < 3 || slots > 8 || engine_lds_bytes(slots, x->c.hidden, x->c.ffn) > 160 * 1024)
-      MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3..8 and fit the CU's 160 KB of LDS");
+    if (depth != 2 && depth != 3) MX_FAIL(x, MX_ERR_ARG, "engine_depth must be 2 or 3");
+    if (slots < 3 || slots > 8 || slots <= depth ||
+        engine_lds_bytes(slots, x->c.hidden, x->c.ffn) > 160 * 1024)
+      MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3..8, above engine_depth, and fit the CU's 160 KB of LDS");
     if (en) {
       const auto& c = x->c;
       MX_TRY(x, hipSetDevice(x->device));
@@ -1116,11 +1119,15 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
                                "multiples of 1024, <= 31 layers, GQA <= 4)");
       EngineArgs ea = engine_args(x);
       ea.ring_slots = slots;
+      ea.depth = depth;
+      if (c.heads / c.kv_heads < 3)
+        MX_FAIL(x, MX_ERR_ARG, "b1_engine: instantiated for GQA 3 (Orpheus) and 4 only");
       MX_TRY(x, engine_per_cu(ea, &per_cu));
       if (per_cu < 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine: a workgroup does not fit one CU");
       x->engine_grid = cus;  // one per CU, all co-resident (every wait is also time-bounded)
     }
     x->engine_slots = slots;
+    x->engine_depth = depth;
     x->b1_engine = en ? 1 : 0;
   } else if (k == "head_b1") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_b1 must be 0 or 1");

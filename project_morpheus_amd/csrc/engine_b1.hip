@@ -45,7 +45,6 @@ namespace eng {
 constexpr int NC = 4;                // consumer waves
 constexpr int NT = 64 * (NC + 1);    // workgroup threads
 constexpr int SLOT = 16384;          // ring slot bytes
-constexpr int DEPTH = 2;             // ring slots the loader keeps in flight
 constexpr int SL = 128;              // attention split length (positions; 4 waves x 32)
 enum { PH_QKV = 0, PH_ATT = 1, PH_H1 = 2, PH_ACT = 3, PH_H2 = 4 };
 
@@ -134,7 +133,11 @@ __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :
 // vmcnt <= n, for the in-flight counts the schedule produces (slots of 12 / 16 instructions,
 // DEPTH newer slots); any other n waits for the largest listed count below it
 __device__ __forceinline__ void wait_vm_n(int n) {
-  if (n >= 32) wait_vm<32>();
+  if (n >= 48) wait_vm<48>();
+  else if (n >= 44) wait_vm<44>();
+  else if (n >= 40) wait_vm<40>();
+  else if (n >= 36) wait_vm<36>();
+  else if (n >= 32) wait_vm<32>();
   else if (n >= 28) wait_vm<28>();
   else if (n >= 24) wait_vm<24>();
   else if (n >= 16) wait_vm<16>();
@@ -279,7 +282,8 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
-template <bool F8, int GRP>
+// DEPTH: ring slots the loader keeps in flight beyond the one it waits for
+template <bool F8, int GRP, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int NS = a.ring_slots;
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
   if (wid == 0) {
     // ================================ LOADER ================================
     int k = 0, pend_lo = 0;  // slots [pend_lo, k) issued, not yet published
-    int ips1 = 0, ips2 = 0;  // instructions of the newest two issued slots (k - 1, k - 2)
+    int ips1 = 0, ips2 = 0, ips3 = 0;  // instructions of the newest issued slots (k - 1, k - 2, k - 3)
     int spins = 0;
     bool dead = false;
     auto publish_all = [&]() {
@@ -344,11 +348,12 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           const size_t off = min(off0 + (size_t)i * 1024, lim);
           __builtin_amdgcn_global_load_lds((gbl_cvoid*)(Wl + off), (lds_void*)(dst + i * 1024), 16, 0, 2);
         }
+        ips3 = ips2;
         ips2 = ips1;
         ips1 = P.ips;
         ++k;
         if (k - pend_lo > DEPTH) {  // the oldest pending slot has landed once only the DEPTH newer remain
-          wait_vm_n(ips1 + ips2);
+          wait_vm_n(ips1 + ips2 + (DEPTH > 2 ? ips3 : 0));
           lds_st(&ctl->ready[pend_lo % NS], pend_lo + 1);
           ++pend_lo;
         }
@@ -799,14 +804,21 @@ size_t engine_lds_bytes(int ring_slots, int H, int F) {
 }
 
 // Workgroups of the engine one CU holds at once (it needs exactly one per CU, all co-resident)
-hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
-  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+static const void* engine_fn(const EngineArgs& a) {
   const int grp = a.heads / a.kv_heads;
   const void* fn = nullptr;
-#define MX_ENGF(F8_, G_) if (a.f8 == F8_ && grp == G_) fn = reinterpret_cast<const void*>(&eng::engine_kernel<F8_, G_>);
-  MX_ENGF(false, 3) MX_ENGF(true, 3) MX_ENGF(false, 2) MX_ENGF(true, 2)
-  MX_ENGF(false, 4) MX_ENGF(true, 4) MX_ENGF(false, 1) MX_ENGF(true, 1)
+#define MX_ENGF(F8_, G_, D_)                                                  \
+  if (a.f8 == F8_ && grp == G_ && a.depth == D_)                              \
+    fn = reinterpret_cast<const void*>(&eng::engine_kernel<F8_, G_, D_>);
+  MX_ENGF(false, 3, 2) MX_ENGF(true, 3, 2) MX_ENGF(false, 4, 2) MX_ENGF(true, 4, 2)
+  MX_ENGF(false, 3, 3) MX_ENGF(true, 3, 3) MX_ENGF(false, 4, 3) MX_ENGF(true, 4, 3)
 #undef MX_ENGF
+  return fn;
+}
+
+hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
+  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+  const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
@@ -814,19 +826,15 @@ hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
 }
 
 hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
-  const int grp = a.heads / a.kv_heads;
   const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
-  if (a.ring_slots < 3 || a.ring_slots > 8 || lds > 160 * 1024 || a.layers > 31) return hipErrorInvalidValue;
-  if (a.H % 1024 || a.F % 1024 || a.heads * 128 != a.H || grp < 1 || grp > 4) return hipErrorNotSupported;
-#define MX_ENG(F8_, G_)                                                                       \
-  if (a.f8 == F8_ && grp == G_) {                                                             \
-    hipLaunchKernelGGL((eng::engine_kernel<F8_, G_>), dim3(grid), dim3(eng::NT), lds, st, a);  \
-    return hipGetLastError();                                                                  \
-  }
-  MX_ENG(false, 3) MX_ENG(true, 3) MX_ENG(false, 2) MX_ENG(true, 2)
-  MX_ENG(false, 4) MX_ENG(true, 4) MX_ENG(false, 1) MX_ENG(true, 1)
-#undef MX_ENG
-  return hipErrorNotSupported;
+  if (a.ring_slots < 3 || a.ring_slots > 8 || a.ring_slots <= a.depth || lds > 160 * 1024 ||
+      a.layers > 31)
+    return hipErrorInvalidValue;
+  if (a.H % 1024 || a.F % 1024 || a.heads * 128 != a.H) return hipErrorNotSupported;
+  const void* fn = engine_fn(a);
+  if (!fn) return hipErrorNotSupported;
+  void* args[] = {const_cast<EngineArgs*>(&a)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(eng::NT), args, lds, st);
 }
 
 }  // namespace mx
