@@ -107,9 +107,15 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
- * flight, 2 or 3).  Drops
+ * flight, 2 or 3), "engine_trace" (record the engine's phase timeline).  Drops
  * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
+/* Diagnostic (option engine_trace on): after a device sync, copy the last engine launch's
+ * timeline, 12 stamps of the 100 MHz clock per (CU, layer) -- consumer: layer start, input
+ * ready, qkv done, attention done, o input ready, o done, gate/up input ready, gate/up done,
+ * down input ready, down done; loader: layer start, layer streamed -- into host_out
+ * ([grid][layers][12], n entries available); *grid_out = the engine's grid. */
+int mx_llm_engine_trace(mx_llm* ctx, uint64_t* host_out, int n, int* grid_out);
 /* Roofline probe: mean microseconds per launch of the decode GEMV/GEMM `which` (0 qkv,
  * 1 o-proj, 2 gate/up, 3 down, 4 the one-row o-proj merging 8 attention splits, 5 lm_head +
  * penalty + argmax) for `n_rows` rows (1..max_batch), timed over one hipGraph of

@@ -151,6 +151,7 @@ struct mx_llm {
   uint32_t* eng_epoch = nullptr;
   int* eng_status_h = nullptr;  // host-mapped status word of the last engine launches
   int* eng_status_d = nullptr;
+  uint64_t* eng_trace = nullptr;  // option engine_trace: per-CU, per-layer phase stamps
   // every layer's matrices / norms / fp8 scales of one kind are contiguous
   void *wqkv_all = nullptr, *wo_all = nullptr, *wgu_all = nullptr, *wd_all = nullptr;
   float *sqkv_all = nullptr, *so_all = nullptr, *sgu_all = nullptr, *sd_all = nullptr;
@@ -779,6 +780,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
   a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth;
   a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
+  a.trace = x->eng_trace;
   return a;
 }
 
@@ -1129,6 +1131,14 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     x->engine_slots = slots;
     x->engine_depth = depth;
     x->b1_engine = en ? 1 : 0;
+  } else if (k == "engine_trace") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "engine_trace must be 0 or 1");
+    if (value && !x->eng_trace) {
+      MX_TRY(x, hipSetDevice(x->device));
+      MX_TRY(x, x->alloc(&x->eng_trace, (size_t)1024 * x->c.layers * 12));
+      MX_TRY(x, hipMemset(x->eng_trace, 0, (size_t)1024 * x->c.layers * 12 * 8));
+    }
+    if (!value) x->eng_trace = nullptr;  // (the buffer stays allocated until destroy)
   } else if (k == "head_b1") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_b1 must be 0 or 1");
     x->head_b1 = value;
@@ -1220,6 +1230,18 @@ extern "C" int mx_llm_row_state(const mx_llm* x, int row, int* active, int* next
 }
 
 extern "C" int32_t* mx_llm_history(mx_llm* x) { return x ? x->hist_host : nullptr; }
+
+extern "C" int mx_llm_engine_trace(mx_llm* x, uint64_t* host_out, int n, int* grid_out) {
+  if (!x || !host_out || !grid_out) return MX_ERR_ARG;
+  if (!x->eng_trace) MX_FAIL(x, MX_ERR_STATE, "engine_trace is off");
+  const size_t need = (size_t)x->engine_grid * x->c.layers * 12;
+  if ((size_t)n < need) MX_FAIL(x, MX_ERR_ARG, "trace buffer too small");
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, hipDeviceSynchronize());
+  MX_TRY(x, hipMemcpy(host_out, x->eng_trace, need * 8, hipMemcpyDeviceToHost));
+  *grid_out = x->engine_grid;
+  return MX_OK;
+}
 
 extern "C" int mx_llm_debug_logits(mx_llm* x, int enable) {
   if (!x) return MX_ERR_ARG;

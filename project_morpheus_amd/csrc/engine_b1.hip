@@ -302,6 +302,10 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
   const uint32_t epoch = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Clock clk{__builtin_amdgcn_s_memrealtime() + (uint64_t)a.timeout_ticks};
 
+  // optional timeline (option engine_trace): 12 stamps of the 100 MHz clock per (CU, layer)
+  auto stamp = [&](int l, int idx) {
+    if (a.trace) a.trace[((size_t)c * a.layers + l) * 12 + idx] = __builtin_amdgcn_s_memrealtime();
+  };
   if (tid < 8) {
     ctl->ready[tid] = 0;
     ctl->freed[tid] = 0;
@@ -360,10 +364,12 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       }
     };
     for (int l = 0; l < a.layers && !dead; ++l) {
+      if (lane == 0) stamp(l, 10);
       stream_phase(ph0, l);
       if (!dead) stream_phase(ph1, l);
       if (!dead) stream_phase(ph2, l);
       if (!dead) stream_phase(ph3, l);
+      if (lane == 0) stamp(l, 11);
     }
     publish_all();
     if (dead) lds_st(&ctl->abort_, 1);
@@ -401,6 +407,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       const uint32_t tg = (epoch << 8) | ((uint32_t)l << 3);
       uint16_t* kc = a.kcache + a.kv_layer_elems * l;
       uint16_t* vc = a.vcache + a.kv_layer_elems * l;
+      const bool st0 = ct == 0;
+      if (st0) stamp(l, 0);
       // ---------------- QKV ----------------
       {
         // this layer's e4m3 row scales and (once) the rope factors of the step's position, to
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         ss = wave_sum(ss);
         if (lane == 0) ctl->ss[cw] = ss;
         if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+        if (st0) stamp(l, 1);
         const float scale = 1.0f / sqrtf((ctl->ss[0] + ctl->ss[1] + ctl->ss[2] + ctl->ss[3]) / H + a.eps);
         const Ph& P = ph0;
         const int pos = L - 1;
@@ -491,6 +500,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           }
         }
         if (!ok) break;
+        if (st0) stamp(l, 2);
       }
       // ---------------- ATTENTION ----------------
       for (int it = 0; it < items; ++it) {
@@ -694,12 +704,14 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         if (!(ok = cbar(ctl, gen, clk, a.status))) break;  // scratch reused by the next item
       }
       if (!ok) break;
+      if (st0) stamp(l, 3);
       // ---------------- O-PROJ ----------------
       {
         float ss;
         ok = gather<EPC>(a.g_att, QD, tg + PH_ATT, Xb, KC_Q, nullptr, nullptr, 0, 0, ct, ss, ctl,
                          clk, a.status);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
+        if (st0) stamp(l, 4);
         const Ph& P = ph1;
         for (int s = 0; s < P.nslots; ++s, ++k) {
           if (k % NC != cw) continue;
@@ -719,6 +731,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           }
         }
         if (!ok) break;
+        if (st0) stamp(l, 5);
       }
       // ---------------- GATE / UP ----------------
       {
@@ -729,6 +742,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         ss = wave_sum(ss);
         if (lane == 0) ctl->ss[cw] = ss;
         if (!(ok = cbar(ctl, gen, clk, a.status))) break;
+        if (st0) stamp(l, 6);
         const float scale = 1.0f / sqrtf((ctl->ss[0] + ctl->ss[1] + ctl->ss[2] + ctl->ss[3]) / H + a.eps);
         const Ph& P = ph2;
         for (int s = 0; s < P.nslots; ++s, ++k) {
@@ -752,6 +766,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           }
         }
         if (!ok) break;
+        if (st0) stamp(l, 7);
       }
       // ---------------- DOWN ----------------
       {
@@ -759,6 +774,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         ok = gather<EPC>(a.g_act, F, tg + PH_ACT, Xb, KC_F, nullptr, nullptr, 0, 0, ct, ss, ctl, clk,
                          a.status);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
+        if (st0) stamp(l, 8);
         const Ph& P = ph3;
         const bool last_layer = l == a.layers - 1;
         for (int s = 0; s < P.nslots; ++s, ++k) {
@@ -779,6 +795,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           }
         }
         if (!ok) break;
+        if (st0) stamp(l, 9);
       }
     }
     if (!ok) lds_st(&ctl->abort_, 1);

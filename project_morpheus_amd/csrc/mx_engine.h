@@ -24,6 +24,7 @@ struct EngineArgs {
   int depth;                               // ring slots in flight (2 or 3)
   float eps;
   long long timeout_ticks;                 // 100 MHz realtime ticks per launch
+  uint64_t* trace;                         // null, or [grid][layers][12] clock stamps
 };
 
 size_t engine_lds_bytes(int ring_slots, int H, int F);

@@ -126,6 +126,16 @@ class LlmEngine:
                                                     C.byref(us)))
         return us.value
 
+    def engine_trace(self) -> np.ndarray:
+        """Timeline of the last persistent-engine launch (option engine_trace): clock stamps
+        (100 MHz) [grid][layers][12], see include/morpheus_mx.h mx_llm_engine_trace."""
+        n = 1024 * self.cfg.layers * 12
+        buf = (C.c_uint64 * n)()
+        grid = C.c_int(0)
+        self._check(self.lib.mx_llm_engine_trace(self.h, buf, n, C.byref(grid)))
+        arr = np.frombuffer(buf, dtype=np.uint64, count=grid.value * self.cfg.layers * 12)
+        return arr.reshape(grid.value, self.cfg.layers, 12).copy()
+
     def set_option(self, key: str, value: int) -> None:
         self._check(self.lib.mx_llm_set_option(self.h, key.encode(), int(value)))
 
