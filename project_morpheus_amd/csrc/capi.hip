@@ -779,6 +779,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.layers = c.layers; a.H = c.hidden; a.heads = c.heads; a.kv_heads = c.kv_heads; a.F = c.ffn;
   a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
   a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth;
+  a.xb = engine_xb_floats(c.heads, c.kv_heads, c.ffn);
   a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
   a.trace = x->eng_trace;
   return a;
@@ -1104,7 +1105,7 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     if (k == "b1_engine" && value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine must be 0 or 1");
     if (depth != 2 && depth != 3) MX_FAIL(x, MX_ERR_ARG, "engine_depth must be 2 or 3");
     if (slots < 3 || slots > 8 || slots <= depth ||
-        engine_lds_bytes(slots, x->c.hidden, x->c.ffn) > 160 * 1024)
+        engine_lds_bytes(slots, x->c.hidden, engine_xb_floats(x->c.heads, x->c.kv_heads, x->c.ffn)) > 160 * 1024)
       MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3..8, above engine_depth, and fit the CU's 160 KB of LDS");
     if (en) {
       const auto& c = x->c;

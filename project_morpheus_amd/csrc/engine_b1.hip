@@ -39,6 +39,8 @@
 #include "mx_llm_kernels.h"
 #include "mx_engine.h"
 
+#include <algorithm>
+
 namespace mx {
 namespace eng {
 
@@ -46,6 +48,9 @@ constexpr int NC = 4;                // consumer waves
 constexpr int NT = 64 * (NC + 1);    // workgroup threads
 constexpr int SLOT = 16384;          // ring slot bytes
 constexpr int SL = 128;              // attention split length (positions; 4 waves x 32)
+constexpr int RING_MAX = 7;          // ring slots (LDS: 112 KB)
+constexpr int XA_MAX = 3072;         // staged hidden-width activation (floats)
+constexpr int XB_MAX = 8192;         // staged ffn-width activation / attention scratch (floats)
 enum { PH_QKV = 0, PH_ATT = 1, PH_H1 = 2, PH_ACT = 3, PH_H2 = 4 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -78,6 +83,35 @@ __device__ __forceinline__ int lds_ld(const int* p) {
 }
 __device__ __forceinline__ void lds_st(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Ring flags: relaxed LDS accesses with compiler-only fences.  A release / acquire at
+// workgroup scope makes the compiler wait for EVERY outstanding vector-memory operation of the
+// wave (vmcnt(0)), which would drain the loader's in-flight LDS-DMA at each publish; the
+// ordering is explicit instead: the loader publishes a slot after a counted vmcnt wait (its
+// DMA has landed), and LDS instructions of one wave execute in order.
+__device__ __forceinline__ int ring_ld(const int* p) {
+  const int v = __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+  return v;
+}
+__device__ __forceinline__ void ring_st(int* p, int v) {
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// The loader's own flag accesses, as inline asm: with LDS-DMA in flight the compiler puts a
+// vmcnt(0) in front of any LDS instruction it emits (it cannot tell the flag from the DMA
+// target), which would drain the weight stream at every publish.  The loader's DMA targets are
+// the ring slots only, never these words.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
+}
+__device__ __forceinline__ int loader_ld(const int* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+  return v;
+}
+__device__ __forceinline__ void loader_st(int* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
 
 struct Ctl {           // LDS control block
@@ -285,12 +319,15 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
 // DEPTH: ring slots the loader keeps in flight beyond the one it waits for
 template <bool F8, int GRP, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // Separate LDS objects (not one dynamic array): the compiler then knows the ring flags and
+  // the staged activations do not alias the LDS-DMA target, and does not drain the loader's
+  // in-flight DMA (vmcnt(0)) before every flag write.
+  __shared__ __attribute__((aligned(16))) uint8_t ring[RING_MAX * SLOT];
+  __shared__ __attribute__((aligned(16))) float Xa[XA_MAX];
+  __shared__ __attribute__((aligned(16))) float Xb[XB_MAX];
+  __shared__ Ctl ctl_s;
+  Ctl* ctl = &ctl_s;
   const int NS = a.ring_slots;
-  uint8_t* ring = smem;
-  float* Xa = reinterpret_cast<float*>(smem + (size_t)NS * SLOT);         // H floats
-  float* Xb = Xa + a.H;                                                    // max(F, QD) floats
-  Ctl* ctl = reinterpret_cast<Ctl*>(Xb + a.F);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = gridDim.x, c = blockIdx.x;
   constexpr int esz = F8 ? 1 : 2;
@@ -328,7 +365,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
     bool dead = false;
     auto publish_all = [&]() {
       wait_vm<0>();
-      for (int q = pend_lo; q < k; ++q) lds_st(&ctl->ready[q % NS], q + 1);
+      for (int q = pend_lo; q < k; ++q) loader_st(&ctl->ready[q % NS], q + 1);
       pend_lo = k;
     };
     auto stream_phase = [&](const Ph& P, int l) {
@@ -336,11 +373,11 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       const size_t lim = P.layer_bytes - 16;
       for (int s = 0; s < P.nslots; ++s) {
         const int pos = k % NS;
-        if (k >= NS && lds_ld(&ctl->freed[pos]) != k - NS + 1) {
+        if (k >= NS && loader_ld(&ctl->freed[pos]) != k - NS + 1) {
           publish_all();
-          while (lds_ld(&ctl->freed[pos]) != k - NS + 1) {
+          while (loader_ld(&ctl->freed[pos]) != k - NS + 1) {
             __builtin_amdgcn_s_sleep(2);
-            if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+            if ((++spins & 255) == 0 && (loader_ld(&ctl->abort_) || clk.expired())) {
               dead = true;
               return;
             }
@@ -358,7 +395,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         ++k;
         if (k - pend_lo > DEPTH) {  // the oldest pending slot has landed once only the DEPTH newer remain
           wait_vm_n(ips1 + ips2 + (DEPTH > 2 ? ips3 : 0));
-          lds_st(&ctl->ready[pend_lo % NS], pend_lo + 1);
+          loader_st(&ctl->ready[pend_lo % NS], pend_lo + 1);
           ++pend_lo;
         }
       }
@@ -391,7 +428,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
     auto take = [&](int kk) -> const uint4* {
       const int pos = kk % NS;
       int spins = 0;
-      while (lds_ld(&ctl->ready[pos]) != kk + 1) {
+      while (ring_ld(&ctl->ready[pos]) != kk + 1) {
         __builtin_amdgcn_s_sleep(1);
         if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
           lds_st(&ctl->abort_, 1);
@@ -401,7 +438,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       }
       return reinterpret_cast<const uint4*>(ring + (size_t)pos * SLOT);
     };
-    auto give = [&](int kk) { lds_st(&ctl->freed[kk % NS], kk + 1); };
+    // (slot_dot's LDS reads have returned: their values are in the reduced sums)
+    auto give = [&](int kk) { ring_st(&ctl->freed[kk % NS], kk + 1); };
 
     for (int l = 0; l < a.layers && ok; ++l) {
       const uint32_t tg = (epoch << 8) | ((uint32_t)l << 3);
@@ -461,7 +499,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, F8 ? 4 : 2>(sl, Xa4, KC_H, nr, lane, acc);
+          slot_dot<F8, 4>(sl, Xa4, KC_H, nr, lane, acc);
           give(k);
           if (lane == 0) {
             for (int j = 0; j + 1 < nr; j += 2) {
@@ -719,7 +757,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, F8 ? 4 : 2>(sl, Xb4, KC_Q, nr, lane, acc);
+          slot_dot<F8, 4>(sl, Xb4, KC_Q, nr, lane, acc);
           give(k);
           if (lane < nr) {
             float y = acc[0];
@@ -751,7 +789,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, F8 ? 4 : 2>(sl, Xa4, KC_H, nr, lane, acc);
+          slot_dot<F8, 4>(sl, Xa4, KC_H, nr, lane, acc);
           give(k);
           // pair j (rows n0 + 2j, n0 + 2j + 1) -> lane j
           if (2 * lane + 1 < nr) {
@@ -782,11 +820,13 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           const uint4* sl = take(k);
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
-          float acc[2];
-          slot_dot<F8, F8 ? 2 : 1>(sl, Xb4, KC_F, nr, lane, acc);
+          float acc[4];
+          slot_dot<F8, 4>(sl, Xb4, KC_F, nr, lane, acc);
           give(k);
           if (lane < nr) {
-            float y = lane == 0 ? acc[0] : acc[F8 ? 1 : 0];
+            float y = acc[0];
+#pragma unroll
+            for (int j = 1; j < 4; ++j) y = lane == j ? acc[j] : y;
             const int n = n0 + lane;
             if (F8) y *= ctl->scl[l & 1][SC_D + n - P.r0];
             const float v = ctl->res2[n - P.r0] + y;
@@ -816,8 +856,16 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
 
 }  // namespace eng
 
-size_t engine_lds_bytes(int ring_slots, int H, int F) {
-  return (size_t)ring_slots * eng::SLOT + (size_t)(H + F) * 4 + sizeof(eng::Ctl);
+// Xb holds the o-proj input (heads x 128), the down-proj input (ffn) and the attention scratch
+int engine_xb_floats(int heads, int kv_heads, int F) {
+  const int grp = heads / kv_heads;
+  const int att = grp * 128 + 256 + (eng::NC + 1) * grp * 130;
+  return std::max(std::max(F, heads * 128), att);
+}
+// the engine's LDS is static (eng::RING_MAX slots, XA_MAX / XB_MAX floats): shapes must fit it
+size_t engine_lds_bytes(int ring_slots, int H, int xb_floats) {
+  if (ring_slots > eng::RING_MAX || H > eng::XA_MAX || xb_floats > eng::XB_MAX) return ~(size_t)0;
+  return (size_t)eng::RING_MAX * eng::SLOT + (size_t)(eng::XA_MAX + eng::XB_MAX) * 4 + sizeof(eng::Ctl);
 }
 
 // Workgroups of the engine one CU holds at once (it needs exactly one per CU, all co-resident)
@@ -834,16 +882,15 @@ static const void* engine_fn(const EngineArgs& a) {
 }
 
 hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
-  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.xb);
   const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (e != hipSuccess) return e;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, eng::NT, lds);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, eng::NT, 0);
 }
 
 hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
-  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.F);
+  const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.xb);
   if (a.ring_slots < 3 || a.ring_slots > 8 || a.ring_slots <= a.depth || lds > 160 * 1024 ||
       a.layers > 31)
     return hipErrorInvalidValue;
@@ -851,7 +898,7 @@ hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
   const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;
   void* args[] = {const_cast<EngineArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(eng::NT), args, lds, st);
+  return hipLaunchKernel(fn, dim3(grid), dim3(eng::NT), args, 0, st);
 }
 
 }  // namespace mx

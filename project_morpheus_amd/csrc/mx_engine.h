@@ -22,12 +22,14 @@ struct EngineArgs {
   int* status;                             // host-mapped: 0, or why a launch gave up
   int layers, H, heads, kv_heads, F, max_pos, smax, ring_slots, f8;
   int depth;                               // ring slots in flight (2 or 3)
+  int xb;                                  // floats of the second staging buffer (engine_xb_floats)
   float eps;
   long long timeout_ticks;                 // 100 MHz realtime ticks per launch
   uint64_t* trace;                         // null, or [grid][layers][12] clock stamps
 };
 
-size_t engine_lds_bytes(int ring_slots, int H, int F);
+int engine_xb_floats(int heads, int kv_heads, int F);
+size_t engine_lds_bytes(int ring_slots, int H, int xb_floats);
 // engine workgroups one CU holds (sets the kernel's dynamic-LDS limit; call outside capture)
 hipError_t engine_per_cu(const EngineArgs& a, int* per_cu);
 hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st);
