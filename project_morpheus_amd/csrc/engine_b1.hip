@@ -262,6 +262,13 @@ __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, floa
   return true;
 }
 
+// Before a gather: poll one WITNESS granule per producer (the last of its contiguous range of
+// `per` outputs) instead of sweeping the whole vector, so 256 CUs waiting on an edge put ~4 KB
+// each per poll round on the fabric, not the vector (24-64 KB); then join the consumer barrier.
+// The sweep that follows is then almost always one pass.
+__device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t tag, int ct,
+                                        Ctl* ctl, int& gen, const Clock& clk, int* status);
+
 // Dot products of the rows of one ring slot with the staged activation: rows j < nr of
 // rowbytes each (K = rowbytes / esz); lane handles 16-byte chunks m = lane + 64 i.
 template <bool F8, int RPS>
@@ -296,6 +303,26 @@ __device__ __forceinline__ void slot_dot(const uint4* slot, const float4* X, int
   }
 #pragma unroll
   for (int j = 0; j < RPS; ++j) acc[j] = wave_sum(acc[j]);
+}
+
+__device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t tag, int ct,
+                                        Ctl* ctl, int& gen, const Clock& clk, int* status) {
+  const int nw = (n + per - 1) / per;
+  for (int i = ct; i < nw; i += 256) {
+    const int wi = min((i + 1) * per, n) - 1;
+    int spins = 0;
+    while (true) {
+      const u32x4v v = gget2(g, wi & ~1);
+      if ((wi & 1 ? v.w : v.y) == tag) break;
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+        lds_st(&ctl->abort_, 1);
+        __hip_atomic_store(status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+  }
+  return cbar(ctl, gen, clk, status);
 }
 
 __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, bf16x8& f2) {
@@ -423,6 +450,9 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
     const int S = (L + SL - 1) / SL;
     const int items = S * a.kv_heads;
     const float att_scale = 1.0f / sqrtf(128.0f);
+    // outputs per producer CU of the o / down projections (h1, h2) and of gate/up (act)
+    const int per_h = (H + G - 1) / G;                             // make_ph(.., pair = false)
+    const int per_act = ((((2 * F + G - 1) / G) + 1) & ~1) / 2;    // make_ph(.., pair = true) / 2
 
     // wait for ring slot k; returns its LDS base (nullptr on abort)
     auto take = [&](int kk) -> const uint4* {
@@ -482,7 +512,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
             Xa[((((kk % EPC) >> 2) * KC_H) + kk / EPC) * 4 + (kk & 3)] = x * nw[kk];
           }
         } else {
-          ok = gather<EPC>(a.g_h2, H, tg - 8 + PH_H2, Xa, KC_H, nw, ctl->res1, ph1.r0,
+          ok = witness(a.g_h2, H, per_h, tg - 8 + PH_H2, ct, ctl, gen, clk, a.status) &&
+               gather<EPC>(a.g_h2, H, tg - 8 + PH_H2, Xa, KC_H, nw, ctl->res1, ph1.r0,
                            ph1.r1 - ph1.r0, ct, ss, ctl, clk, a.status);
           if (!ok) break;
         }
@@ -746,7 +777,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- O-PROJ ----------------
       {
         float ss;
-        ok = gather<EPC>(a.g_att, QD, tg + PH_ATT, Xb, KC_Q, nullptr, nullptr, 0, 0, ct, ss, ctl,
+        ok = witness(a.g_att, QD, GRP * 128, tg + PH_ATT, ct, ctl, gen, clk, a.status) &&
+             gather<EPC>(a.g_att, QD, tg + PH_ATT, Xb, KC_Q, nullptr, nullptr, 0, 0, ct, ss, ctl,
                          clk, a.status);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
         if (st0) stamp(l, 4);
@@ -774,7 +806,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- GATE / UP ----------------
       {
         float ss;
-        ok = gather<EPC>(a.g_h1, H, tg + PH_H1, Xa, KC_H, a.mlp_norm + (size_t)l * H, ctl->res2,
+        ok = witness(a.g_h1, H, per_h, tg + PH_H1, ct, ctl, gen, clk, a.status) &&
+             gather<EPC>(a.g_h1, H, tg + PH_H1, Xa, KC_H, a.mlp_norm + (size_t)l * H, ctl->res2,
                          ph3.r0, ph3.r1 - ph3.r0, ct, ss, ctl, clk, a.status);
         if (!ok) break;
         ss = wave_sum(ss);
@@ -809,7 +842,8 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- DOWN ----------------
       {
         float ss;
-        ok = gather<EPC>(a.g_act, F, tg + PH_ACT, Xb, KC_F, nullptr, nullptr, 0, 0, ct, ss, ctl, clk,
+        ok = witness(a.g_act, F, per_act, tg + PH_ACT, ct, ctl, gen, clk, a.status) &&
+             gather<EPC>(a.g_act, F, tg + PH_ACT, Xb, KC_F, nullptr, nullptr, 0, 0, ct, ss, ctl, clk,
                          a.status);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
         if (st0) stamp(l, 8);
