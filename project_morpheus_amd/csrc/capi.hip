@@ -145,6 +145,7 @@ struct mx_llm {
   // persistent one-row engine (engine_b1.hip): option b1_engine runs the layers of a
   // one-row decode step as one launch (engine_slots = its LDS ring depth)
   int b1_engine = 0, engine_slots = 7, engine_depth = 2, engine_grid = 0;
+  int engine_dbg = 0;  // option engine_dbg: timing experiments (outputs invalid when != 0)
   uint2 *g_qkv = nullptr, *g_att = nullptr, *g_h1 = nullptr, *g_act = nullptr, *g_h2 = nullptr;
   float* eng_part = nullptr;
   int* eng_tickets = nullptr;
@@ -782,6 +783,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.xb = engine_xb_floats(c.heads, c.kv_heads, c.ffn);
   a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
   a.trace = x->eng_trace;
+  a.dbg = x->engine_dbg;
   return a;
 }
 
@@ -1132,6 +1134,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     x->engine_slots = slots;
     x->engine_depth = depth;
     x->b1_engine = en ? 1 : 0;
+  } else if (k == "engine_dbg") {
+    if (value < 0 || value > 3) MX_FAIL(x, MX_ERR_ARG, "engine_dbg must be 0..3");
+    x->engine_dbg = value;
   } else if (k == "engine_trace") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "engine_trace must be 0 or 1");
     if (value && !x->eng_trace) {

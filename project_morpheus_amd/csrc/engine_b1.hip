@@ -207,8 +207,10 @@ __device__ __forceinline__ bool cbar(Ctl* ctl, int& gen, const Clock& clk, int* 
 template <int EPC>
 __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, float* X, int KC,
                                        const float* w, float* res, int rs0, int nres, int ct,
-                                       float& ss, Ctl* ctl, const Clock& clk, int* status) {
+                                       float& ss, Ctl* ctl, const Clock& clk, int* status,
+                                       bool skip = false) {
   ss = 0.f;
+  if (skip) return true;  // timing experiment (EngineArgs::dbg & 1): no hand-off waits
   constexpr int B = 8;  // granule pairs in flight per thread (n <= 4096 in one round)
   for (int base = 2 * ct; base < n; base += 2 * 256 * B) {
     u32x4v v[B];
@@ -267,7 +269,8 @@ __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, floa
 // each per poll round on the fabric, not the vector (24-64 KB); then join the consumer barrier.
 // The sweep that follows is then almost always one pass.
 __device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t tag, int ct,
-                                        Ctl* ctl, int& gen, const Clock& clk, int* status);
+                                        Ctl* ctl, int& gen, const Clock& clk, int* status,
+                                        bool skip);
 
 // Dot products of the rows of one ring slot with the staged activation: rows j < nr of
 // rowbytes each (K = rowbytes / esz); lane handles 16-byte chunks m = lane + 64 i.
@@ -306,7 +309,9 @@ __device__ __forceinline__ void slot_dot(const uint4* slot, const float4* X, int
 }
 
 __device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t tag, int ct,
-                                        Ctl* ctl, int& gen, const Clock& clk, int* status) {
+                                        Ctl* ctl, int& gen, const Clock& clk, int* status,
+                                        bool skip) {
+  if (skip) return cbar(ctl, gen, clk, status);
   const int nw = (n + per - 1) / per;
   for (int i = ct; i < nw; i += 256) {
     const int wi = min((i + 1) * per, n) - 1;
@@ -412,9 +417,11 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         }
         const size_t off0 = (size_t)(P.r0 + s * P.rps) * P.rowbytes + (size_t)lane * 16;
         uint8_t* dst = ring + (size_t)pos * SLOT;
-        for (int i = 0; i < P.ips; ++i) {
-          const size_t off = min(off0 + (size_t)i * 1024, lim);
-          __builtin_amdgcn_global_load_lds((gbl_cvoid*)(Wl + off), (lds_void*)(dst + i * 1024), 16, 0, 2);
+        if (!(a.dbg & 2)) {
+          for (int i = 0; i < P.ips; ++i) {
+            const size_t off = min(off0 + (size_t)i * 1024, lim);
+            __builtin_amdgcn_global_load_lds((gbl_cvoid*)(Wl + off), (lds_void*)(dst + i * 1024), 16, 0, 2);
+          }
         }
         ips3 = ips2;
         ips2 = ips1;
@@ -450,6 +457,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
     const int S = (L + SL - 1) / SL;
     const int items = S * a.kv_heads;
     const float att_scale = 1.0f / sqrtf(128.0f);
+    const bool nodeps = a.dbg & 1;  // timing experiment: stream only, no hand-off waits
     // outputs per producer CU of the o / down projections (h1, h2) and of gate/up (act)
     const int per_h = (H + G - 1) / G;                             // make_ph(.., pair = false)
     const int per_act = ((((2 * F + G - 1) / G) + 1) & ~1) / 2;    // make_ph(.., pair = true) / 2
@@ -512,9 +520,9 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
             Xa[((((kk % EPC) >> 2) * KC_H) + kk / EPC) * 4 + (kk & 3)] = x * nw[kk];
           }
         } else {
-          ok = witness(a.g_h2, H, per_h, tg - 8 + PH_H2, ct, ctl, gen, clk, a.status) &&
+          ok = witness(a.g_h2, H, per_h, tg - 8 + PH_H2, ct, ctl, gen, clk, a.status, nodeps) &&
                gather<EPC>(a.g_h2, H, tg - 8 + PH_H2, Xa, KC_H, nw, ctl->res1, ph1.r0,
-                           ph1.r1 - ph1.r0, ct, ss, ctl, clk, a.status);
+                           ph1.r1 - ph1.r0, ct, ss, ctl, clk, a.status, nodeps);
           if (!ok) break;
         }
         ss = wave_sum(ss);
@@ -572,7 +580,7 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         if (st0) stamp(l, 2);
       }
       // ---------------- ATTENTION ----------------
-      for (int it = 0; it < items; ++it) {
+      for (int it = 0; it < (nodeps ? 0 : items); ++it) {
         // item it = (kv head, split) runs on CU it * G / items (spread over the grid)
         if (it * G / items != c) continue;
         const int kvh = it % a.kv_heads, sp = it / a.kv_heads;
@@ -605,14 +613,14 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
         {
           float dummy;
           ok = gather<4>(a.g_qkv + (size_t)kvh * GRP * 128, GRP * 128, tg + PH_QKV, qs, GRP * 32,
-                         nullptr, nullptr, 0, 0, ct, dummy, ctl, clk, a.status);
+                         nullptr, nullptr, 0, 0, ct, dummy, ctl, clk, a.status, nodeps);
           // (EPC 4: plane 0 only, i.e. qs[k] in natural order)
           if (ok && has_new) {
             ok = gather<4>(a.g_qkv + QD + kvh * 128, 128, tg + PH_QKV, kn, 32, nullptr, nullptr, 0, 0,
-                           ct, dummy, ctl, clk, a.status);
+                           ct, dummy, ctl, clk, a.status, nodeps);
             if (ok)
               ok = gather<4>(a.g_qkv + QD + KVD + kvh * 128, 128, tg + PH_QKV, vn, 32, nullptr, nullptr,
-                             0, 0, ct, dummy, ctl, clk, a.status);
+                             0, 0, ct, dummy, ctl, clk, a.status, nodeps);
           }
           if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
         }
@@ -777,9 +785,9 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- O-PROJ ----------------
       {
         float ss;
-        ok = witness(a.g_att, QD, GRP * 128, tg + PH_ATT, ct, ctl, gen, clk, a.status) &&
+        ok = witness(a.g_att, QD, GRP * 128, tg + PH_ATT, ct, ctl, gen, clk, a.status, nodeps) &&
              gather<EPC>(a.g_att, QD, tg + PH_ATT, Xb, KC_Q, nullptr, nullptr, 0, 0, ct, ss, ctl,
-                         clk, a.status);
+                         clk, a.status, nodeps);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
         if (st0) stamp(l, 4);
         const Ph& P = ph1;
@@ -806,9 +814,9 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- GATE / UP ----------------
       {
         float ss;
-        ok = witness(a.g_h1, H, per_h, tg + PH_H1, ct, ctl, gen, clk, a.status) &&
+        ok = witness(a.g_h1, H, per_h, tg + PH_H1, ct, ctl, gen, clk, a.status, nodeps) &&
              gather<EPC>(a.g_h1, H, tg + PH_H1, Xa, KC_H, a.mlp_norm + (size_t)l * H, ctl->res2,
-                         ph3.r0, ph3.r1 - ph3.r0, ct, ss, ctl, clk, a.status);
+                         ph3.r0, ph3.r1 - ph3.r0, ct, ss, ctl, clk, a.status, nodeps);
         if (!ok) break;
         ss = wave_sum(ss);
         if (lane == 0) ctl->ss[cw] = ss;
@@ -842,9 +850,9 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
       // ---------------- DOWN ----------------
       {
         float ss;
-        ok = witness(a.g_act, F, per_act, tg + PH_ACT, ct, ctl, gen, clk, a.status) &&
+        ok = witness(a.g_act, F, per_act, tg + PH_ACT, ct, ctl, gen, clk, a.status, nodeps) &&
              gather<EPC>(a.g_act, F, tg + PH_ACT, Xb, KC_F, nullptr, nullptr, 0, 0, ct, ss, ctl, clk,
-                         a.status);
+                         a.status, nodeps);
         if (!ok || !(ok = cbar(ctl, gen, clk, a.status))) break;
         if (st0) stamp(l, 8);
         const Ph& P = ph3;

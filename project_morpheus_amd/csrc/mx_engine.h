@@ -26,6 +26,7 @@ struct EngineArgs {
   float eps;
   long long timeout_ticks;                 // 100 MHz realtime ticks per launch
   uint64_t* trace;                         // null, or [grid][layers][12] clock stamps
+  int dbg;                                 // timing experiments only: 1 no hand-off waits, 2 no weight DMA
 };
 
 int engine_xb_floats(int heads, int kv_heads, int F);

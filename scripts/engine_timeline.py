@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--slots", type=int, default=7)
     ap.add_argument("--depth", type=int, default=2)
+    ap.add_argument("--dbg", type=int, default=0, help="1: no hand-off waits, 2: no weight stream")
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -40,6 +41,7 @@ def main():
     llm.set_option("engine_depth", args.depth)
     llm.set_option("b1_engine", 1)
     llm.set_option("engine_trace", 1)
+    llm.set_option("engine_dbg", args.dbg)
     st = torch.cuda.Stream()
     prompt = list(range(1000, 1020))
     llm.prefill(0, 0, prompt, 1.1, st)
@@ -50,7 +52,8 @@ def main():
     G, Lyr, _ = tr.shape
     t0 = tr[:, 0, 10].min()
     us = (tr - t0) / 100.0                       # 100 MHz -> µs
-    out = {"pos": args.pos, "fp8": args.fp8, "slots": args.slots, "depth": args.depth, "grid": G,
+    out = {"pos": args.pos, "fp8": args.fp8, "slots": args.slots, "depth": args.depth,
+           "dbg": args.dbg, "grid": G,
            "step_us": float(us[:, -1, 9].max()), "layers": []}
     for l in range(Lyr):
         row = {"layer": l, "start_med": round(float(np.median(us[:, l, 0])), 2)}
@@ -64,12 +67,12 @@ def main():
     out["mid_layer_median"] = {k: round(float(np.median([r[k] for r in mids])), 2)
                                for k in PHASES + ["layer_med", "loader_stream"]}
     print(json.dumps(out["mid_layer_median"]))
-    print(json.dumps({k: out[k] for k in ("pos", "fp8", "slots", "depth", "grid", "step_us")}))
+    print(json.dumps({k: out[k] for k in ("pos", "fp8", "slots", "depth", "dbg", "grid", "step_us")}))
     for r in out["layers"][:3] + out["layers"][-2:]:
         print(json.dumps(r))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"engine_timeline_{'fp8' if args.fp8 else 'bf16'}"
-                           f"_p{args.pos}_s{args.slots}_d{args.depth}.json"), "w") as fh:
+                           f"_p{args.pos}_s{args.slots}_d{args.depth}_x{args.dbg}.json"), "w") as fh:
         json.dump(out, fh)
     llm.close()
 
