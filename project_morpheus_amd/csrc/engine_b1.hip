@@ -272,40 +272,92 @@ __device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t
                                         Ctl* ctl, int& gen, const Clock& clk, int* status,
                                         bool skip);
 
-// Dot products of the rows of one ring slot with the staged activation: rows j < nr of
-// rowbytes each (K = rowbytes / esz); lane handles 16-byte chunks m = lane + 64 i.
-template <bool F8, int RPS>
-__device__ __forceinline__ void slot_dot(const uint4* slot, const float4* X, int KC, int nr,
-                                         int lane, float* acc) {
+// 64-lane sum: the four in-row steps on DPP (quad_perm [1,0,3,2], [2,3,0,1], row_ror 4, 8:
+// VALU, no LDS round trip), the two cross-row steps as lane shuffles
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  v += dpp<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x128>(v);  // row_ror:8
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// Dot products of the rows of one ring slot with the staged activation: rows j < nr of the
+// slot (RPS per slot, KCL 16-byte chunks per lane per row; row j's chunk m at slot[j KC + m],
+// lane takes m = lane + 64 i).  Every LDS read of a batch of CH chunks is issued before any
+// FMA (one LDS round trip per batch, not per chunk); rows past nr re-read row nr - 1 and are
+// ignored by the caller.
+template <bool F8, int RPS, int KCL>
+__device__ __forceinline__ float4 slot_dot_t(const uint4* slot, const float4* X, int KC, int nr,
+                                             int lane) {
   constexpr int PL = F8 ? 4 : 2;
+  constexpr int CH = F8 ? (KCL < 4 ? KCL : 4) : (KCL < 8 ? KCL : 8);
+  static_assert(KCL % CH == 0, "chunk batches");
+  float acc[RPS];
 #pragma unroll
   for (int j = 0; j < RPS; ++j) acc[j] = 0.f;
-  for (int m = lane; m < KC; m += 64) {
-    float4 xq[PL];
 #pragma unroll
-    for (int q = 0; q < PL; ++q) xq[q] = X[q * KC + m];
+  for (int c0 = 0; c0 < KCL; c0 += CH) {
+    float4 xq[CH][PL];
+    uint4 w[CH][RPS];
 #pragma unroll
-    for (int j = 0; j < RPS; ++j) {
-      if (j >= nr) break;
-      const uint4 w = slot[j * KC + m];
-      if (F8) {
-        const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+    for (int i = 0; i < CH; ++i) {
+      const int m = lane + 64 * (c0 + i);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
-          const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
-          acc[j] = fmaf(lo.x, xq[q].x, acc[j]);
-          acc[j] = fmaf(lo.y, xq[q].y, acc[j]);
-          acc[j] = fmaf(hi.x, xq[q].z, acc[j]);
-          acc[j] = fmaf(hi.y, xq[q].w, acc[j]);
+      for (int q = 0; q < PL; ++q) xq[i][q] = X[q * KC + m];
+#pragma unroll
+      for (int j = 0; j < RPS; ++j) w[i][j] = slot[min(j, nr - 1) * KC + m];
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+#pragma unroll
+      for (int j = 0; j < RPS; ++j) {
+        if (F8) {
+          const uint32_t wd[4] = {w[i][j].x, w[i][j].y, w[i][j].z, w[i][j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], false);
+            const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(wd[q], true);
+            acc[j] = fmaf(lo.x, xq[i][q].x, acc[j]);
+            acc[j] = fmaf(lo.y, xq[i][q].y, acc[j]);
+            acc[j] = fmaf(hi.x, xq[i][q].z, acc[j]);
+            acc[j] = fmaf(hi.y, xq[i][q].w, acc[j]);
+          }
+        } else {
+          acc[j] = dot8(w[i][j], xq[i][0], xq[i][1], acc[j]);
         }
-      } else {
-        acc[j] = dot8(w, xq[0], xq[1], acc[j]);
       }
     }
   }
+  float out[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < RPS; ++j) acc[j] = wave_sum(acc[j]);
+  for (int j = 0; j < RPS; ++j) out[j] = wave_sum_fast(acc[j]);
+  return make_float4(out[0], out[1], out[2], out[3]);
+}
+
+// the (rows per slot, chunks per lane) pairs of the engine's shapes: bf16 K 3072 / 8192 and
+// fp8 K 3072 / 8192 (Orpheus-3B), bf16 / fp8 K 1024 / 2048 (the small parity shape)
+// (not inlined: its ~100 VGPRs of batched LDS reads would add to the live state of every phase
+// of the consumer loop and push the whole kernel into spills)
+template <bool F8>
+__device__ __noinline__ float4 slot_dot(const uint4* slot, const float4* X, int KC, int nr,
+                                        int rps, int lane) {
+  const int kcl = KC / 64;
+#define MX_SD(R_, K_) \
+  if (rps == R_ && kcl == K_) return slot_dot_t<F8, R_, K_>(slot, X, KC, nr, lane);
+  if constexpr (!F8) {
+    MX_SD(2, 6) MX_SD(1, 16) MX_SD(4, 2) MX_SD(4, 4)
+  } else {
+    MX_SD(4, 3) MX_SD(2, 8) MX_SD(4, 1) MX_SD(4, 2)
+  }
+#undef MX_SD
+  return make_float4(0.f, 0.f, 0.f, 0.f);  // (no other shape passes the host-side check)
 }
 
 __device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t tag, int ct,
@@ -538,7 +590,10 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, 4>(sl, Xa4, KC_H, nr, lane, acc);
+          {
+            const float4 r4 = slot_dot<F8>(sl, Xa4, KC_H, nr, P.rps, lane);
+            acc[0] = r4.x; acc[1] = r4.y; acc[2] = r4.z; acc[3] = r4.w;
+          }
           give(k);
           if (lane == 0) {
             for (int j = 0; j + 1 < nr; j += 2) {
@@ -797,7 +852,10 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, 4>(sl, Xb4, KC_Q, nr, lane, acc);
+          {
+            const float4 r4 = slot_dot<F8>(sl, Xb4, KC_Q, nr, P.rps, lane);
+            acc[0] = r4.x; acc[1] = r4.y; acc[2] = r4.z; acc[3] = r4.w;
+          }
           give(k);
           if (lane < nr) {
             float y = acc[0];
@@ -830,7 +888,10 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, 4>(sl, Xa4, KC_H, nr, lane, acc);
+          {
+            const float4 r4 = slot_dot<F8>(sl, Xa4, KC_H, nr, P.rps, lane);
+            acc[0] = r4.x; acc[1] = r4.y; acc[2] = r4.z; acc[3] = r4.w;
+          }
           give(k);
           // pair j (rows n0 + 2j, n0 + 2j + 1) -> lane j
           if (2 * lane + 1 < nr) {
@@ -863,7 +924,10 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
           if (!sl) { ok = false; break; }
           const int n0 = P.r0 + s * P.rps, nr = min(P.rps, P.r1 - n0);
           float acc[4];
-          slot_dot<F8, 4>(sl, Xb4, KC_F, nr, lane, acc);
+          {
+            const float4 r4 = slot_dot<F8>(sl, Xb4, KC_F, nr, P.rps, lane);
+            acc[0] = r4.x; acc[1] = r4.y; acc[2] = r4.z; acc[3] = r4.w;
+          }
           give(k);
           if (lane < nr) {
             float y = acc[0];
