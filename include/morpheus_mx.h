@@ -107,7 +107,7 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
- * flight, 2 or 3), "engine_trace" (record the engine's phase timeline), "engine_dbg" (timing
+ * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline), "engine_dbg" (timing
  * experiments: 1 = no hand-off waits, 2 = no weight stream; outputs invalid).  Drops
  * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);

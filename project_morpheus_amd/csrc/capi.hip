@@ -144,7 +144,7 @@ struct mx_llm {
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent one-row engine (engine_b1.hip): option b1_engine runs the layers of a
   // one-row decode step as one launch (engine_slots = its LDS ring depth)
-  int b1_engine = 0, engine_slots = 7, engine_depth = 2, engine_grid = 0;
+  int b1_engine = 0, engine_slots = 7, engine_depth = 2, engine_loaders = 2, engine_grid = 0;
   int engine_dbg = 0;  // option engine_dbg: timing experiments (outputs invalid when != 0)
   uint2 *g_qkv = nullptr, *g_att = nullptr, *g_h1 = nullptr, *g_act = nullptr, *g_h2 = nullptr;
   float* eng_part = nullptr;
@@ -779,7 +779,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.part = x->eng_part; a.tickets = x->eng_tickets; a.epoch = x->eng_epoch; a.status = x->eng_status_d;
   a.layers = c.layers; a.H = c.hidden; a.heads = c.heads; a.kv_heads = c.kv_heads; a.F = c.ffn;
   a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
-  a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth;
+  a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth; a.loaders = x->engine_loaders;
   a.xb = engine_xb_floats(c.heads, c.kv_heads, c.ffn);
   a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
   a.trace = x->eng_trace;
@@ -1100,6 +1100,14 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_mt") {
     if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "rows_head_mt must be 1 or 2");
     x->rows_head_mt = value;
+  } else if (k == "engine_loaders") {
+    if (value != 1 && value != 2) MX_FAIL(x, MX_ERR_ARG, "engine_loaders must be 1 or 2");
+    x->engine_loaders = value;
+    if (x->b1_engine) {
+      int per_cu = 0;
+      MX_TRY(x, engine_per_cu(engine_args(x), &per_cu));
+      if (per_cu < 1) MX_FAIL(x, MX_ERR_ARG, "engine_loaders: a workgroup does not fit one CU");
+    }
   } else if (k == "b1_engine" || k == "engine_slots" || k == "engine_depth") {
     const bool en = k == "b1_engine" ? value != 0 : x->b1_engine != 0;
     const int slots = k == "engine_slots" ? value : x->engine_slots;

@@ -44,8 +44,7 @@
 namespace mx {
 namespace eng {
 
-constexpr int NC = 4;                // consumer waves
-constexpr int NT = 64 * (NC + 1);    // workgroup threads
+constexpr int NC = 4;                // consumer waves (after the NL loader waves)
 constexpr int SLOT = 16384;          // ring slot bytes
 constexpr int SL = 128;              // attention split length (positions; 4 waves x 32)
 constexpr int RING_MAX = 7;          // ring slots (LDS: 112 KB)
@@ -400,9 +399,11 @@ __device__ __forceinline__ void split3(const float* x, bf16x8& f0, bf16x8& f1, b
 // ---------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------
-// DEPTH: ring slots the loader keeps in flight beyond the one it waits for
-template <bool F8, int GRP, int DEPTH>
-__global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
+// NL loader waves (slot k streamed by loader k mod NL), each keeping a.depth slots in flight
+// beyond the one it waits for: one wave's 63-instruction vmcnt window (~63 KB) is below the
+// bytes in flight a CU needs at the loaded-chip latency
+template <bool F8, int GRP, int NL>
+__global__ __launch_bounds__(64 * (NC + NL), 1) void engine_kernel(EngineArgs a) {
   // Separate LDS objects (not one dynamic array): the compiler then knows the ring flags and
   // the staged activations do not alias the LDS-DMA target, and does not drain the loader's
   // in-flight DMA (vmcnt(0)) before every flag write.
@@ -441,21 +442,22 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
   const Ph ph0 = make_ph(a.wqkv, QKVN, H, esz, G, c, true), ph1 = make_ph(a.wo, H, QD, esz, G, c, false),
            ph2 = make_ph(a.wgu, 2 * F, H, esz, G, c, true), ph3 = make_ph(a.wd, H, F, esz, G, c, false);
 
-  if (wid == 0) {
+  if (wid < NL) {
     // ================================ LOADER ================================
-    int k = 0, pend_lo = 0;  // slots [pend_lo, k) issued, not yet published
-    int ips1 = 0, ips2 = 0, ips3 = 0;  // instructions of the newest issued slots (k - 1, k - 2, k - 3)
+    const int DEPTH = a.depth;
+    int k = 0;
+    int kq[4], iq[4], qh = 0, qn = 0;  // this loader's issued, unpublished slots (oldest first)
     int spins = 0;
     bool dead = false;
     auto publish_all = [&]() {
       wait_vm<0>();
-      for (int q = pend_lo; q < k; ++q) loader_st(&ctl->ready[q % NS], q + 1);
-      pend_lo = k;
+      for (; qn > 0; --qn, qh = (qh + 1) & 3) loader_st(&ctl->ready[kq[qh] % NS], kq[qh] + 1);
     };
     auto stream_phase = [&](const Ph& P, int l) {
       const uint8_t* Wl = P.W + (size_t)l * P.layer_bytes;
       const size_t lim = P.layer_bytes - 16;
-      for (int s = 0; s < P.nslots; ++s) {
+      for (int s = 0; s < P.nslots; ++s, ++k) {
+        if (k % NL != wid) continue;
         const int pos = k % NS;
         if (k >= NS && loader_ld(&ctl->freed[pos]) != k - NS + 1) {
           publish_all();
@@ -475,30 +477,33 @@ __global__ __launch_bounds__(NT, 1) void engine_kernel(EngineArgs a) {
             __builtin_amdgcn_global_load_lds((gbl_cvoid*)(Wl + off), (lds_void*)(dst + i * 1024), 16, 0, 2);
           }
         }
-        ips3 = ips2;
-        ips2 = ips1;
-        ips1 = P.ips;
-        ++k;
-        if (k - pend_lo > DEPTH) {  // the oldest pending slot has landed once only the DEPTH newer remain
-          wait_vm_n(ips1 + ips2 + (DEPTH > 2 ? ips3 : 0));
-          loader_st(&ctl->ready[pend_lo % NS], pend_lo + 1);
-          ++pend_lo;
+        const int qt = (qh + qn) & 3;
+        kq[qt] = k;
+        iq[qt] = P.ips;
+        ++qn;
+        if (qn > DEPTH) {  // the oldest has landed once only the DEPTH newer are outstanding
+          int newer = 0;
+          for (int j = 1; j < qn; ++j) newer += iq[(qh + j) & 3];
+          wait_vm_n(newer);
+          loader_st(&ctl->ready[kq[qh] % NS], kq[qh] + 1);
+          qh = (qh + 1) & 3;
+          --qn;
         }
       }
     };
     for (int l = 0; l < a.layers && !dead; ++l) {
-      if (lane == 0) stamp(l, 10);
+      if (wid == 0 && lane == 0) stamp(l, 10);
       stream_phase(ph0, l);
       if (!dead) stream_phase(ph1, l);
       if (!dead) stream_phase(ph2, l);
       if (!dead) stream_phase(ph3, l);
-      if (lane == 0) stamp(l, 11);
+      if (wid == 0 && lane == 0) stamp(l, 11);
     }
     publish_all();
     if (dead) lds_st(&ctl->abort_, 1);
   } else {
     // =============================== CONSUMERS ===============================
-    const int cw = wid - 1, ct = tid - 64;
+    const int cw = wid - NL, ct = tid - 64 * NL;
     int gen = 0;
     bool ok = true;
     int k = 0;  // global slot index, same walk as the loader
@@ -978,11 +983,11 @@ size_t engine_lds_bytes(int ring_slots, int H, int xb_floats) {
 static const void* engine_fn(const EngineArgs& a) {
   const int grp = a.heads / a.kv_heads;
   const void* fn = nullptr;
-#define MX_ENGF(F8_, G_, D_)                                                  \
-  if (a.f8 == F8_ && grp == G_ && a.depth == D_)                              \
-    fn = reinterpret_cast<const void*>(&eng::engine_kernel<F8_, G_, D_>);
+#define MX_ENGF(F8_, G_, L_)                                                  \
+  if (a.f8 == F8_ && grp == G_ && a.loaders == L_)                            \
+    fn = reinterpret_cast<const void*>(&eng::engine_kernel<F8_, G_, L_>);
+  MX_ENGF(false, 3, 1) MX_ENGF(true, 3, 1) MX_ENGF(false, 4, 1) MX_ENGF(true, 4, 1)
   MX_ENGF(false, 3, 2) MX_ENGF(true, 3, 2) MX_ENGF(false, 4, 2) MX_ENGF(true, 4, 2)
-  MX_ENGF(false, 3, 3) MX_ENGF(true, 3, 3) MX_ENGF(false, 4, 3) MX_ENGF(true, 4, 3)
 #undef MX_ENGF
   return fn;
 }
@@ -992,7 +997,7 @@ hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
   const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, eng::NT, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, 64 * (eng::NC + a.loaders), 0);
 }
 
 hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
@@ -1004,7 +1009,7 @@ hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
   const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;
   void* args[] = {const_cast<EngineArgs*>(&a)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(eng::NT), args, 0, st);
+  return hipLaunchKernel(fn, dim3(grid), dim3(64 * (eng::NC + a.loaders)), args, 0, st);
 }
 
 }  // namespace mx

@@ -21,7 +21,8 @@ struct EngineArgs {
   uint32_t* epoch;                         // [0] epoch (>= 1), [1] finished-workgroup ticket
   int* status;                             // host-mapped: 0, or why a launch gave up
   int layers, H, heads, kv_heads, F, max_pos, smax, ring_slots, f8;
-  int depth;                               // ring slots in flight (2 or 3)
+  int depth;                               // ring slots in flight per loader wave (2 or 3)
+  int loaders;                             // loader waves (1 or 2)
   int xb;                                  // floats of the second staging buffer (engine_xb_floats)
   float eps;
   long long timeout_ticks;                 // 100 MHz realtime ticks per launch

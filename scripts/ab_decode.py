@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
-            "rows_head_mt": 2, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "b1_engine": 0}
+            "rows_head_mt": 2, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -44,6 +44,8 @@ VARIANTS = {
     "engine_s6": {"b1_engine": 1, "engine_slots": 6},
     "engine_s5": {"b1_engine": 1, "engine_slots": 5},
     "engine_d3": {"b1_engine": 1, "engine_depth": 3},
+    "engine_l1": {"b1_engine": 1, "engine_loaders": 1},
+    "engine_l1d3": {"b1_engine": 1, "engine_loaders": 1, "engine_depth": 3},
     "engine_d3s6": {"b1_engine": 1, "engine_depth": 3, "engine_slots": 6},
 }
 

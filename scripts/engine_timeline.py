@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--slots", type=int, default=7)
     ap.add_argument("--depth", type=int, default=2)
+    ap.add_argument("--loaders", type=int, default=2)
     ap.add_argument("--dbg", type=int, default=0, help="1: no hand-off waits, 2: no weight stream")
     args = ap.parse_args()
     import torch
@@ -39,6 +40,7 @@ def main():
     torch.cuda.empty_cache()
     llm.set_option("engine_slots", args.slots)
     llm.set_option("engine_depth", args.depth)
+    llm.set_option("engine_loaders", args.loaders)
     llm.set_option("b1_engine", 1)
     llm.set_option("engine_trace", 1)
     llm.set_option("engine_dbg", args.dbg)
@@ -72,7 +74,7 @@ def main():
         print(json.dumps(r))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"engine_timeline_{'fp8' if args.fp8 else 'bf16'}"
-                           f"_p{args.pos}_s{args.slots}_d{args.depth}_x{args.dbg}.json"), "w") as fh:
+                           f"_p{args.pos}_s{args.slots}_d{args.depth}_l{args.loaders}_x{args.dbg}.json"), "w") as fh:
         json.dump(out, fh)
     llm.close()
 
