@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1)
     ap.add_argument("--kinds", default="qkv,o_proj,gate_up,down")
     ap.add_argument("--options", default="", help="k=v,k=v set_option knobs")
+    ap.add_argument("--fp8", action="store_true", help="e4m3 weights + per-row scales")
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -25,8 +26,12 @@ def main():
     from project_morpheus_amd.weights import synthetic_llm_weights
     cfg = C.OrpheusConfig()
     w = synthetic_llm_weights(cfg, seed=0, device="cuda:0")
+    if args.fp8:
+        from project_morpheus_amd.weights import quantize_fp8
+        w = quantize_fp8(w, cfg)
     R = args.rows
-    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=64)
+    llm = LlmEngine(cfg, w, device=0, max_slots=R, max_pos=2048, max_batch=R, max_prefill=64,
+                    wdtype="fp8" if args.fp8 else "bf16")
     del w
     torch.cuda.empty_cache()
     for kv in filter(None, args.options.split(",")):
