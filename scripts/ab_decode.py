@@ -40,6 +40,8 @@ VARIANTS = {
     "hmt1": {"rows_head_mt": 1},
     "nohead1": {"head_b1": 0},
     "tmerge": {"rows_merge": 0},
+    "nwb4": {"att_nw_batch": 4},
+    "cpwb2": {"att_cpw_batch": 2},
     "engine": {"b1_engine": 1},
     "engine_s6": {"b1_engine": 1, "engine_slots": 6},
     "engine_s5": {"b1_engine": 1, "engine_slots": 5},
