@@ -20,7 +20,7 @@ from _dispatch import PREFILL_TAG
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # rocprofv3 --kernel-trace --stats of whole default bench runs (scripts/gpu_full.sh)
-BENCH_TRACES = ["profiles/r04_bench_kernel_stats_final.csv"]
+BENCH_TRACES = ["profiles/r04_bench_kernel_stats_final.csv", "profiles/r05_bench_kernel_stats.csv"]
 _LLM = re.compile(r"void mx::((?:v4::gemm_rows|attn|gemv1?|head1::head_b1)_kernel<[^>]*>)"
                   r"\((?:mx::GemvArgs|mx::AttnArgs)\)")
 
