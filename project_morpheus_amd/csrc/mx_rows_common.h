@@ -171,6 +171,10 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
     }
   }
   if (EPI == EPI_ARGMAX) {
+    // one atomic per (block, batch row): the 8 waves' keys meet in LDS first (a per-wave
+    // atomic put 8x the same-address device atomics on each row's key)
+    __shared__ unsigned long long bred[8][16 * NT];
+    const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       unsigned long long k = best[nt];
@@ -179,8 +183,16 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
         const unsigned long long o = __shfl_xor(k, m, 64);
         k = o > k ? o : k;
       }
-      const int b = r0 + 16 * nt + c;
-      if (g == 0 && b < a.R && k) atomicMax(a.best + b, k);
+      if (g == 0) bred[w][16 * nt + c] = k;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < 16 * NT) {
+      unsigned long long k = bred[0][t];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) k = bred[i][t] > k ? bred[i][t] : k;
+      const int b = r0 + t;
+      if (b < a.R && k) atomicMax(a.best + b, k);
     }
   }
 }

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
-            "rows_head_mt": 2, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
+            "rows_head_mt": 2, "rows_head_target": 0, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -42,6 +42,10 @@ VARIANTS = {
     "tmerge": {"rows_merge": 0},
     "nwb4": {"att_nw_batch": 4},
     "cpwb2": {"att_cpw_batch": 2},
+    "ht1024": {"rows_head_target": 1024},
+    "ht2048": {"rows_head_target": 2048},
+    "ht4096": {"rows_head_target": 4096},
+    "hmt1_ht2048": {"rows_head_mt": 1, "rows_head_target": 2048},
     "engine": {"b1_engine": 1},
     "engine_s6": {"b1_engine": 1, "engine_slots": 6},
     "engine_s5": {"b1_engine": 1, "engine_slots": 5},
