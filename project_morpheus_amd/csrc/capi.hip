@@ -137,7 +137,7 @@ struct mx_llm {
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
-  int rows_head_mt = 2;              // option: multi-row lm_head weight rows per wave / 16
+  int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
                                      // (2: -22 us at 32 bf16 rows, -28 us at 8 e4m3 rows)
   int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)

@@ -11,10 +11,11 @@ hipError_t launch_rows_head(const GemvArgs& a, int epi, bool norm, int nt, hipSt
     if (nt == 2) return launch_rows_k<1, 2, EPI_, NORM_>(a, st);                          \
     return launch_rows_k<1, 4, EPI_, NORM_>(a, st);                                       \
   }
-  // rows_head_mt = 2 (the default): 32 weight rows per wave (256 per block), so every staged
-  // activation sub-chunk feeds twice the lm_head weights (half the activation re-reads);
-  // measured -22 us per 32-row bf16 step, -28 us per 8-row e4m3 step
-  // (profiles/r04_ab_small_rows_v1_head_options.log, r04_small_rows_gemv_not_kept.log)
+  // rows_head_mt = 2 (option): 32 weight rows per wave (256 per block), so every staged
+  // activation sub-chunk feeds twice the lm_head weights.  It won round 4 (-22 us per 32-row
+  // bf16 step) only while every wave took its own argmax atomic; with one atomic per block
+  // (rows_epilogue) the 16-row waves at 128 VGPRs (two blocks per CU) stream faster: 8 rows
+  // 169 -> 150 us bf16, 91 -> 80 us e4m3; 32 rows 185 -> 154 us (profiles/r05_head_options.log)
   if (epi == EPI_ARGMAX && norm && a.rows_head_mt == 2) {
     if (nt == 1) return launch_rows_k<2, 1, EPI_ARGMAX, true>(a, st);
     if (nt == 2) return launch_rows_k<2, 2, EPI_ARGMAX, true>(a, st);

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
-            "rows_head_mt": 2, "rows_head_target": 0, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
+            "rows_head_mt": 1, "rows_head_target": 0, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -38,6 +38,7 @@ VARIANTS = {
     "t96": {"rows_target": 96},
     "nw8": {"att_cpw": 1, "att_nw": 8},
     "hmt1": {"rows_head_mt": 1},
+    "hmt2": {"rows_head_mt": 2},
     "nohead1": {"head_b1": 0},
     "tmerge": {"rows_merge": 0},
     "nwb4": {"att_nw_batch": 4},

@@ -15,12 +15,13 @@ sys.path.insert(0, ROOT)
 VARIANTS = {
     "base": {},
     "mt1": {"rows_head_mt": 1},
+    "mt2": {"rows_head_mt": 2},
     "t1024": {"rows_head_target": 1024},
     "t2048": {"rows_head_target": 2048},
     "t4096": {"rows_head_target": 4096},
     "mt1_t2048": {"rows_head_mt": 1, "rows_head_target": 2048},
 }
-DEFAULTS = {"rows_head_mt": 2, "rows_head_target": 0}
+DEFAULTS = {"rows_head_mt": 1, "rows_head_target": 0}
 
 
 def main():

@@ -155,29 +155,30 @@ def probe_keys():
 
 
 def bench_envelope(prompt_len=10, stream_prompts=(16, 64), job_prompts=(22, 259),
-                   max_tokens=1200, batch=32, fp8_batch=8):
+                   max_tokens=1200, batch=32, fp8_batch=8, opts=None):
     """Every (rows, longest span) a default bench.py run can step, at Orpheus widths:
     configs[1] and the HTTP lines (one bf16 row), configs[2] (<= 32 rows, prompts of 16..64
     ids), configs[3] long_read and its 8-GPU rank share (<= 32 rows, the jobs' 22..259-id
     prompts), configs[4] (<= 8 e4m3 rows and one e4m3 row).  Rows x spans are taken as a
-    product (a superset of what one run steps)."""
+    product (a superset of what one run steps).  ``opts``: library options that differ from
+    today's defaults (a trace recorded under an earlier default)."""
     keys = set()
     d = ORPHEUS
     s_lo, s_hi = stream_prompts
     j_lo, j_hi = job_prompts
     for f8 in (False, True):
         for L in range(2, max(prompt_len, s_hi) + max_tokens + 1):
-            keys |= decode_keys(d, 1, L, f8)
+            keys |= decode_keys(d, 1, L, f8, opts)
         for n in [prompt_len] + list(range(s_lo, s_hi + 1)):
-            keys |= prefill_keys(d, n, f8)
+            keys |= prefill_keys(d, n, f8, opts)
     for R in range(2, batch + 1):
         for L in range(s_lo + 1, max(s_hi, j_hi) + max_tokens + 1):
-            keys |= decode_keys(d, R, L, False)
+            keys |= decode_keys(d, R, L, False, opts)
     for n in range(s_lo, j_hi + 1):
-        keys |= prefill_keys(d, n, False)
+        keys |= prefill_keys(d, n, False, opts)
     for n in range(j_lo, s_lo):
-        keys |= prefill_keys(d, n, False)
+        keys |= prefill_keys(d, n, False, opts)
     for R in range(2, fp8_batch + 1):
         for L in range(s_lo + 1, s_hi + max_tokens + 1):
-            keys |= decode_keys(d, R, L, True)
+            keys |= decode_keys(d, R, L, True, opts)
     return keys
