@@ -125,6 +125,13 @@ int mx_llm_engine_trace(mx_llm* ctx, uint64_t* host_out, int n, int* grid_out);
  * slots: only on an idle context. */
 int mx_llm_bench_gemv(mx_llm* ctx, int which, int n_rows, int reps, float* us_out,
                       double* bytes_out);
+/* Diagnostic: per-block phase stamps (s_memrealtime, 100 MHz) of the multi-row GEMM launch of
+ * mx_llm_bench_gemv's last layer, replayed inside its sweep: host_out[block * 8 + k], k = 0
+ * entry, 1 first activation staged, 2 first weight sub-chunk consumed, 3 main loop done,
+ * 4 split-K partial published + ticket, 5 K ranges merged, 6 epilogue done (0 = not
+ * reached).  n_rows >= 2; *blocks_out = grid size (<= cap_blocks). */
+int mx_llm_bench_gemv_trace(mx_llm* ctx, int which, int n_rows, uint64_t* host_out,
+                            int cap_blocks, int* blocks_out);
 /* Diagnostic: mean microseconds of one eager attention launch (layer 0) for n_rows rows of
  * length L, `cpw` 32-position chunks per wave (split = 128*cpw), experiment flags `debug`
  * (0 = product kernel).  Clobbers decode-row state: only on an idle context. */

@@ -1005,8 +1005,8 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
 // residual / KV scratch written are meaningless).  Sweeping every layer keeps the stream
 // out of the 256 MB Infinity Cache, as in a real step.  Writes mean microseconds per
 // launch (inter-kernel gap in the graph included) and the weight bytes of one launch.
-extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, float* us_out,
-                                 double* bytes_out) {
+static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us_out,
+                           double* bytes_out, unsigned long long* trace) {
   if (!x || !us_out || which < 0 || which > 5 || reps < 1) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
@@ -1067,7 +1067,11 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, flo
   MX_TRY(x, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
   hipError_t e = hipSuccess;
   for (int i = 0; i < reps && e == hipSuccess; ++i)
-    for (int li = 0; li < c.layers && e == hipSuccess; ++li) e = launch_gemv(args(li), epi, norm, st);
+    for (int li = 0; li < c.layers && e == hipSuccess; ++li) {
+      GemvArgs g = args(li);
+      if (i == reps - 1 && li == c.layers - 1) g.trace = trace;  // the sweep's last launch
+      e = launch_gemv(g, epi, norm, st);
+    }
   hipError_t e2 = hipStreamEndCapture(st, &g);
   MX_TRY(x, e);
   MX_TRY(x, e2);
@@ -1089,6 +1093,37 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, flo
   *us_out = 1e3f * ms / (reps * c.layers);
   const GemvArgs a0 = args(0);
   if (bytes_out) *bytes_out = (double)x->esz * a0.N * a0.K + (x->esz == 1 ? 4.0 * a0.N : 0.0);
+  return MX_OK;
+}
+
+extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, float* us_out,
+                                 double* bytes_out) {
+  return bench_gemv_impl(x, which, n_rows, reps, us_out, bytes_out, nullptr);
+}
+
+// Diagnostic: the multi-row (generation 4) launch of mx_llm_bench_gemv's last layer, replayed
+// in its sweep, with per-block s_memrealtime stamps (100 MHz): host_out[block * 8 + k], k =
+// 0 entry, 1 first activation sub-chunk staged, 2 first weight sub-chunk consumed, 3 main loop
+// done, 4 partial published + ticket taken (split-K only), 5 K ranges merged (last arriver),
+// 6 epilogue done; 0 = not reached.  *blocks_out = the launch's grid size.
+extern "C" int mx_llm_bench_gemv_trace(mx_llm* x, int which, int n_rows, uint64_t* host_out,
+                                       int cap_blocks, int* blocks_out) {
+  if (!x || !host_out || !blocks_out || cap_blocks < 1 || n_rows < 2) return MX_ERR_ARG;
+  MX_TRY(x, hipSetDevice(x->device));
+  unsigned long long* d = nullptr;
+  const size_t n = (size_t)cap_blocks * 8;
+  MX_TRY(x, hipMalloc(&d, n * 8));
+  hipError_t e = hipMemset(d, 0, n * 8);
+  float us = 0.f;
+  int rc = e == hipSuccess ? bench_gemv_impl(x, which, n_rows, 1, &us, nullptr, d) : MX_ERR_HIP;
+  if (rc == MX_OK) e = hipMemcpy(host_out, d, n * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (rc != MX_OK) return rc;
+  MX_TRY(x, e);
+  int blocks = 0;
+  for (int b = 0; b < cap_blocks; ++b)
+    if (host_out[(size_t)b * 8]) blocks = b + 1;
+  *blocks_out = blocks;
   return MX_OK;
 }
 

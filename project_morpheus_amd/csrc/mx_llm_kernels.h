@@ -41,6 +41,7 @@ struct GemvArgs {
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
+  unsigned long long* trace;  // generation 4 diagnostic: [block][8] phase stamps (null = off)
   int head_b1;             // R = 1 lm_head on the persistent kernel (head_b1.hip; 0 = gemv_kernel)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]

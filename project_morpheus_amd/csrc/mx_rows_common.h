@@ -39,7 +39,49 @@ struct EpiPre {
   float sn[EPI == EPI_QKV ? MT : 1][EPI == EPI_QKV ? NT : 1][2];
   int slot[EPI == EPI_QKV ? NT : 1], pos[EPI == EPI_QKV ? NT : 1];
   float ws[MT][4];                                                      // fp8 row scales
+  // ARGMAX: the rows' slots, penalties, logits flags and `seen` bytes (4 per lane and tile),
+  // loaded inside the last two sub-chunks of the main loop (argmax_slots / argmax_operands)
+  int aslot[EPI == EPI_ARGMAX ? NT : 1];
+  float apen[EPI == EPI_ARGMAX ? NT : 1];
+  int akeep[EPI == EPI_ARGMAX ? NT : 1];
+  uint32_t aseen[EPI == EPI_ARGMAX ? MT : 1][EPI == EPI_ARGMAX ? NT : 1];
 };
+
+// The lm_head epilogue's operands hang off the row's slot (row_slot -> seen / penalty): two
+// dependent round trips that a block used to pay after its main loop (p50 9.4 us of a 41 us
+// block at 8 rows, profiles/r05_rows_block_trace.log).  The slot loads go out at the top of
+// sub-chunk SUB - 2, the dependent loads at the top of SUB - 1 (behind every weight load, so
+// vmcnt stays exact), both under the last sub-chunks' weight latency.
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void argmax_slots(const GemvArgs& a, EpiPre<MT, NT, EPI>& P, int r0, int c) {
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    P.aslot[nt % (EPI == EPI_ARGMAX ? NT : 1)] = a.row_slot[min(r0 + 16 * nt + c, a.R - 1)];
+}
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void argmax_operands(const GemvArgs& a, EpiPre<MT, NT, EPI>& P, int n0, int g) {
+  constexpr int ANT = EPI == EPI_ARGMAX ? NT : 1, AMT = EPI == EPI_ARGMAX ? MT : 1;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int slot = P.aslot[nt % ANT];
+    P.apen[nt % ANT] = a.penalty[slot];
+    P.akeep[nt % ANT] = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
+    const uint8_t* seen = a.seen + (size_t)slot * a.N;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int nb = n0 + 16 * mt + 4 * g;
+      uint32_t v = 0;
+      if ((a.N & 3) == 0) {
+        v = *reinterpret_cast<const uint32_t*>(seen + min(nb, a.N - 4));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (nb + i < a.N) v |= (uint32_t)seen[nb + i] << (8 * i);
+      }
+      P.aseen[mt % AMT][nt % ANT] = v;
+    }
+  }
+}
 
 template <int MT, int NT, int EPI>
 __device__ __forceinline__ void rows_epilogue_pre(const GemvArgs& a, EpiPre<MT, NT, EPI>& P,
@@ -153,16 +195,16 @@ __device__ __forceinline__ void rows_epilogue(const GemvArgs& a, f32x4 (&acc)[MT
           }
         }
       } else if (EPI == EPI_ARGMAX) {
-        const int slot = a.row_slot[b];
-        const uint8_t* seen = a.seen + (size_t)slot * a.N;
-        const float pen = a.penalty[slot];
-        const bool keep = a.logits && (a.logits_all || a.samp_temp[slot] > 0.f);
+        constexpr int ANT = EPI == EPI_ARGMAX ? NT : 1, AMT = EPI == EPI_ARGMAX ? MT : 1;
+        const float pen = P.apen[nt % ANT];
+        const bool keep = P.akeep[nt % ANT];
+        const uint32_t sn = P.aseen[mt % AMT][nt % ANT];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int n = nb + i;
           if (n >= a.N) continue;
           float x = v[i];
-          if (seen[n]) x = x > 0.f ? x / pen : x * pen;
+          if ((sn >> (8 * i)) & 0xffu) x = x > 0.f ? x / pen : x * pen;
           if (keep) a.logits[(size_t)b * a.N + n] = x;
           const unsigned long long key = argmax_key(x, (uint32_t)n);
           best[nt] = key > best[nt] ? key : best[nt];

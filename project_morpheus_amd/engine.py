@@ -119,6 +119,16 @@ class LlmEngine:
                                                C.byref(us), C.byref(nb)))
         return us.value, nb.value
 
+    def bench_gemv_trace(self, which: str, n_rows: int, cap_blocks: int = 2048) -> np.ndarray:
+        """Per-block phase stamps [blocks][8] (100 MHz clock) of one multi-row launch of
+        ``which`` (include/morpheus_mx.h mx_llm_bench_gemv_trace)."""
+        buf = (C.c_uint64 * (cap_blocks * 8))()
+        nb = C.c_int(0)
+        self._check(self.lib.mx_llm_bench_gemv_trace(self.h, self.GEMV_KINDS[which], n_rows, buf,
+                                                     cap_blocks, C.byref(nb)))
+        arr = np.frombuffer(buf, dtype=np.uint64, count=nb.value * 8)
+        return arr.reshape(nb.value, 8).copy()
+
     def bench_attention(self, L: int, n_rows: int = 1, cpw: int = 1, debug: int = 0,
                         reps: int = 200) -> float:
         us = C.c_float(0.0)
