@@ -129,7 +129,9 @@ int mx_llm_bench_gemv(mx_llm* ctx, int which, int n_rows, int reps, float* us_ou
  * mx_llm_bench_gemv's last layer, replayed inside its sweep: host_out[block * 8 + k], k = 0
  * entry, 1 first activation staged, 2 first weight sub-chunk consumed, 3 main loop done,
  * 4 split-K partial published + ticket, 5 K ranges merged, 6 epilogue done (0 = not
- * reached).  n_rows >= 2; *blocks_out = grid size (<= cap_blocks). */
+ * reached).  n_rows >= 2; *blocks_out = grid size (<= cap_blocks).  The stamps exist only in
+ * the diagnostic build (MORPHEUS_MX_ROWS_TRACE=1, libmorpheus_mx_trace.so); the product
+ * library returns MX_ERR_STATE. */
 int mx_llm_bench_gemv_trace(mx_llm* ctx, int which, int n_rows, uint64_t* host_out,
                             int cap_blocks, int* blocks_out);
 /* Diagnostic: mean microseconds of one eager attention launch (layer 0) for n_rows rows of

@@ -11,8 +11,13 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.path.join(HERE, "libmorpheus_mx.so")
-OBJ_DIR = os.path.join(CSRC, "build")  # per-translation-unit objects (git-ignored)
+# MORPHEUS_MX_ROWS_TRACE=1 builds the diagnostic variant libmorpheus_mx_trace.so (multi-row
+# GEMM phase stamps, mx_llm_bench_gemv_trace; load it with MORPHEUS_MX_LIB) in its own object
+# directory; the product library never carries the stamps (they cost 1-4 % per step)
+TRACE = os.environ.get("MORPHEUS_MX_ROWS_TRACE", "0") == "1"
+LIB = os.path.join(HERE, "libmorpheus_mx_trace.so" if TRACE else "libmorpheus_mx.so")
+OBJ_DIR = os.path.join(CSRC, "build_trace" if TRACE else "build")  # objects (git-ignored)
+DEFS = ["-DMX_ROWS_TRACE=1"] if TRACE else []
 SOURCES = ["capi.hip", "llm_kernels.hip", "rows_v4_dispatch.hip", "rows_v4_qkv.hip",
            "rows_v4_resid.hip", "rows_v4_silu.hip", "rows_v4_head.hip", "head_b1.hip",
            "sample_kernels.hip", "snac_kernels.hip", "engine_b1.hip"]
@@ -74,7 +79,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if not force and not _stale(s):
             continue
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-               "-munsafe-fp-atomics", "-Wno-unused-result", "-x", "hip", "-c",
+               "-munsafe-fp-atomics", "-Wno-unused-result"] + DEFS + ["-x", "hip", "-c",
                os.path.join(CSRC, s), "-o", _obj(s) + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -1124,6 +1124,9 @@ extern "C" int mx_llm_bench_gemv_trace(mx_llm* x, int which, int n_rows, uint64_
   for (int b = 0; b < cap_blocks; ++b)
     if (host_out[(size_t)b * 8]) blocks = b + 1;
   *blocks_out = blocks;
+  if (!blocks)
+    MX_FAIL(x, MX_ERR_STATE, "no stamps: the library was built without MX_ROWS_TRACE "
+                             "(MORPHEUS_MX_ROWS_TRACE=1 python -m project_morpheus_amd.build)");
   return MX_OK;
 }
 

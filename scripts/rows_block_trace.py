@@ -6,7 +6,10 @@ Each kind's last-layer launch inside an all-layer hipGraph sweep records s_memre
 (100 MHz) per block (include/morpheus_mx.h mx_llm_bench_gemv_trace).  Prints, per (rows, kind),
 times in µs from the earliest block entry: the launch span, block entry spread, first weight
 sub-chunk consumed, main loop end, split-K publish + ticket, last-arriver merge, epilogue end
-(medians and maxima over blocks), and the weight-stream rate of the main loops."""
+(medians and maxima over blocks).  Needs the diagnostic library:
+
+    MORPHEUS_MX_ROWS_TRACE=1 python -m project_morpheus_amd.build
+    MORPHEUS_MX_LIB=project_morpheus_amd/libmorpheus_mx_trace.so python scripts/rows_block_trace.py"""
 import argparse
 import json
 import os
