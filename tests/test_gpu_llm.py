@@ -366,6 +366,20 @@ def test_batched_decode_40_rows_small():
     assert _compare_rows(cfg, w, prompts, 6) >= 0.8 * 40 * 6
 
 
+@pytest.mark.parametrize("vocab", [1003, 1002])
+def test_batched_decode_vocab_not_multiple_of_4_small(vocab):
+    """The multi-row lm_head gathers each row's `seen` flags for its 4 weight rows per lane as
+    one dword when the vocabulary is a multiple of 4 (every shipped shape) and byte by byte
+    otherwise (mx_rows_common.h argmax_operands).  5 rows whose prompts repeat the last 40 ids
+    of the vocabulary put the repetition penalty on the partial last 4-row group (vocab
+    1,003: 3 rows; 1,002: 2)."""
+    cfg = C.OrpheusConfig(hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024, vocab=vocab)
+    w = synthetic_llm_weights(cfg, seed=51, std=0.05, norm_jitter=0.5)
+    rng = np.random.default_rng(vocab)
+    prompts = [[int(x) for x in rng.integers(vocab - 40, vocab, 12 + 3 * i)] for i in range(5)]
+    assert _compare_rows(cfg, w, prompts, 10) >= 0.8 * 5 * 10
+
+
 @pytest.mark.parametrize("cpw", [0, 3, 6, 8])
 def test_batched_attention_chunk_counts_long_ragged(cpw):
     """Multi-row attention with several 32-position chunks per wave: ragged contexts of
