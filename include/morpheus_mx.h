@@ -134,6 +134,11 @@ int mx_llm_bench_gemv(mx_llm* ctx, int which, int n_rows, int reps, float* us_ou
  * library returns MX_ERR_STATE. */
 int mx_llm_bench_gemv_trace(mx_llm* ctx, int which, int n_rows, uint64_t* host_out,
                             int cap_blocks, int* blocks_out);
+/* Diagnostic: mx_llm_bench_gemv's all-layer multi-row sweep (n_rows >= 2; which 0-3, 5)
+ * replayed on nstreams (1..4) streams at once, each with its own split-K workspace (values
+ * meaningless): wall microseconds per launch of one stream's sweep. */
+int mx_llm_bench_gemv_streams(mx_llm* ctx, int which, int n_rows, int reps, int nstreams,
+                              float* us_out);
 /* Diagnostic: mean microseconds of one eager attention launch (layer 0) for n_rows rows of
  * length L, `cpw` 32-position chunks per wave (split = 128*cpw), experiment flags `debug`
  * (0 = product kernel).  Clobbers decode-row state: only on an idle context. */

@@ -65,6 +65,8 @@ _SIGS = {
     "mx_llm_decode_profiled": (C.c_int, [_P, C.c_int, _P, C.POINTER(C.c_double), C.c_int]),
     "mx_llm_set_option": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "mx_llm_engine_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_int)]),
+    "mx_llm_bench_gemv_streams": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(C.c_float)]),
     "mx_llm_bench_gemv_trace": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.c_int,
                                           C.POINTER(C.c_int)]),
     "mx_llm_bench_gemv": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float),

@@ -11,13 +11,17 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-# MORPHEUS_MX_ROWS_TRACE=1 builds the diagnostic variant libmorpheus_mx_trace.so (multi-row
-# GEMM phase stamps, mx_llm_bench_gemv_trace; load it with MORPHEUS_MX_LIB) in its own object
-# directory; the product library never carries the stamps (they cost 1-4 % per step)
+# Diagnostic variants, each its own library and object directory (load one with
+# MORPHEUS_MX_LIB): MORPHEUS_MX_ROWS_TRACE=1 -> libmorpheus_mx_trace.so (multi-row GEMM phase
+# stamps, mx_llm_bench_gemv_trace; the product library never carries them: 1-4 % per step);
+# MORPHEUS_MX_VARIANT=<name> with MORPHEUS_MX_DEFS="-D..." -> libmorpheus_mx_<name>.so
+# (build-time experiment knobs such as MX_ROWS_NP, MX_ROWS_WLOAD_PLAIN)
 TRACE = os.environ.get("MORPHEUS_MX_ROWS_TRACE", "0") == "1"
-LIB = os.path.join(HERE, "libmorpheus_mx_trace.so" if TRACE else "libmorpheus_mx.so")
-OBJ_DIR = os.path.join(CSRC, "build_trace" if TRACE else "build")  # objects (git-ignored)
-DEFS = ["-DMX_ROWS_TRACE=1"] if TRACE else []
+VARIANT = "trace" if TRACE else os.environ.get("MORPHEUS_MX_VARIANT", "")
+LIB = os.path.join(HERE, f"libmorpheus_mx_{VARIANT}.so" if VARIANT else "libmorpheus_mx.so")
+OBJ_DIR = os.path.join(CSRC, f"build_{VARIANT}" if VARIANT else "build")  # objects (git-ignored)
+DEFS = (["-DMX_ROWS_TRACE=1"] if TRACE else []) + \
+    (os.environ.get("MORPHEUS_MX_DEFS", "").split() if VARIANT and not TRACE else [])
 SOURCES = ["capi.hip", "llm_kernels.hip", "rows_v4_dispatch.hip", "rows_v4_qkv.hip",
            "rows_v4_resid.hip", "rows_v4_silu.hip", "rows_v4_head.hip", "head_b1.hip",
            "sample_kernels.hip", "snac_kernels.hip", "engine_b1.hip"]

@@ -1101,6 +1101,115 @@ extern "C" int mx_llm_bench_gemv(mx_llm* x, int which, int n_rows, int reps, flo
   return bench_gemv_impl(x, which, n_rows, reps, us_out, bytes_out, nullptr);
 }
 
+// Diagnostic: the same all-layer sweep of GEMV `which` replayed on `nstreams` streams at once
+// (each with its own split-K workspace and tickets; the activations and outputs are shared
+// scratch, so the values are meaningless): do concurrent row groups overlap each other's ramps
+// and seams, and do they share the weight stream through the Infinity Cache?  Writes the wall
+// time per launch of one stream's sweep.
+extern "C" int mx_llm_bench_gemv_streams(mx_llm* x, int which, int n_rows, int reps,
+                                         int nstreams, float* us_out) {
+  if (!x || !us_out || which < 0 || which > 5 || which == 4 || reps < 1 || nstreams < 1 ||
+      nstreams > 4)
+    return MX_ERR_ARG;
+  if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
+  const auto& c = x->c;
+  if (n_rows < 2 || n_rows > c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows (multi-row only)");
+  MX_TRY(x, hipSetDevice(x->device));
+  const int H = c.hidden, QD = c.heads * 128;
+  {
+    std::vector<int32_t> slots(n_rows), pos(n_rows, 0);
+    for (int i = 0; i < n_rows; ++i) slots[i] = i % c.max_slots;
+    MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
+    MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
+  }
+  std::vector<float*> ws(nstreams, nullptr);
+  std::vector<int*> tk(nstreams, nullptr);
+  std::vector<hipStream_t> sts(nstreams, nullptr);
+  std::vector<hipGraphExec_t> ex(nstreams, nullptr);
+  hipGraph_t gr = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<hipEvent_t> done(nstreams, nullptr);
+  hipError_t e = hipSuccess;
+  for (int s = 0; s < nstreams && e == hipSuccess; ++s) {
+    e = hipMalloc(&ws[s], std::max<size_t>(x->rows_ws_floats, 1) * 4);
+    if (e == hipSuccess) e = hipMalloc(&tk[s], x->rows_tickets_n * 4);
+    if (e == hipSuccess) e = hipMemset(tk[s], 0, x->rows_tickets_n * 4);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sts[s], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&done[s]);
+  }
+  auto args = [&](int li, int s) {
+    const LayerW& l = x->L[li];
+    GemvArgs g{};
+    attach_ws(x, g);
+    g.ws = ws[s];
+    g.tickets = tk[s];
+    g.R = n_rows; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
+    g.row_slot = x->row_slot; g.row_pos = x->row_pos;
+    if (which == 0) {
+      g.W = l.wqkv; g.Wf = x->rows_frag ? l.wqkv_f : nullptr; g.wscale = l.sqkv; g.wdtype = c.wdtype;
+      g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
+      g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.kcache = x->kcache; g.vcache = x->vcache;
+      g.heads = c.heads; g.kv_heads = c.kv_heads; g.max_pos = c.max_pos; g.Q = x->q;
+    } else if (which == 1) {
+      g.W = l.wo; g.Wf = x->rows_frag ? l.wo_f : nullptr; g.wscale = l.so; g.wdtype = c.wdtype;
+      g.N = H; g.K = QD; g.X = x->att; g.Y = x->h_dec;
+    } else if (which == 2) {
+      g.W = l.wgu; g.Wf = x->rows_frag ? l.wgu_f : nullptr; g.wscale = l.sgu; g.wdtype = c.wdtype;
+      g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
+    } else if (which == 3) {
+      g.W = l.wd; g.Wf = x->rows_frag ? l.wd_f : nullptr; g.wscale = l.sd; g.wdtype = c.wdtype;
+      g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->h_dec;
+    } else {
+      g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype;
+      g.N = c.vocab; g.K = H; g.X = x->h_dec; g.norm_w = x->norm;
+      g.seen = x->seen; g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = x->best;
+    }
+    g.xstride = g.K; g.ystride = g.N;
+    return g;
+  };
+  const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : which == 5 ? EPI_ARGMAX : EPI_RESID;
+  const bool norm = which == 0 || which == 2 || which == 5;
+  for (int s = 0; s < nstreams && e == hipSuccess; ++s) {
+    hipGraph_t g = nullptr;
+    e = hipStreamBeginCapture(sts[s], hipStreamCaptureModeRelaxed);
+    for (int i = 0; i < reps && e == hipSuccess; ++i)
+      for (int li = 0; li < c.layers && e == hipSuccess; ++li) e = launch_gemv(args(li, s), epi, norm, sts[s]);
+    const hipError_t e2 = hipStreamEndCapture(sts[s], &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&ex[s], g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  (void)gr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  for (int s = 0; s < nstreams && e == hipSuccess; ++s) e = hipGraphLaunch(ex[s], sts[s]);  // warm
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipEventRecord(e0, sts[0]);
+  for (int s = 1; s < nstreams && e == hipSuccess; ++s) e = hipStreamWaitEvent(sts[s], e0, 0);
+  for (int s = 0; s < nstreams && e == hipSuccess; ++s) e = hipGraphLaunch(ex[s], sts[s]);
+  for (int s = 1; s < nstreams && e == hipSuccess; ++s) {
+    e = hipEventRecord(done[s], sts[s]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(sts[0], done[s], 0);
+  }
+  if (e == hipSuccess) e = hipEventRecord(e1, sts[0]);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  (void)hipDeviceSynchronize();
+  for (int s = 0; s < nstreams; ++s) {
+    if (ex[s]) (void)hipGraphExecDestroy(ex[s]);
+    if (sts[s]) (void)hipStreamDestroy(sts[s]);
+    if (done[s]) (void)hipEventDestroy(done[s]);
+    if (ws[s]) (void)hipFree(ws[s]);
+    if (tk[s]) (void)hipFree(tk[s]);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  MX_TRY(x, e);
+  *us_out = 1e3f * ms / (reps * c.layers);
+  return MX_OK;
+}
+
 // Diagnostic: the multi-row (generation 4) launch of mx_llm_bench_gemv's last layer, replayed
 // in its sweep, with per-block s_memrealtime stamps (100 MHz): host_out[block * 8 + k], k =
 // 0 entry, 1 first activation sub-chunk staged, 2 first weight sub-chunk consumed, 3 main loop

@@ -119,6 +119,14 @@ class LlmEngine:
                                                C.byref(us), C.byref(nb)))
         return us.value, nb.value
 
+    def bench_gemv_streams(self, which: str, n_rows: int, nstreams: int, reps: int = 2) -> float:
+        """µs per launch of one stream's all-layer sweep with ``nstreams`` concurrent copies
+        (include/morpheus_mx.h mx_llm_bench_gemv_streams)."""
+        us = C.c_float(0.0)
+        self._check(self.lib.mx_llm_bench_gemv_streams(self.h, self.GEMV_KINDS[which], n_rows,
+                                                       reps, nstreams, C.byref(us)))
+        return us.value
+
     def bench_gemv_trace(self, which: str, n_rows: int, cap_blocks: int = 2048) -> np.ndarray:
         """Per-block phase stamps [blocks][8] (100 MHz clock) of one multi-row launch of
         ``which`` (include/morpheus_mx.h mx_llm_bench_gemv_trace)."""
