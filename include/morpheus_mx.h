@@ -104,7 +104,7 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
 /* Tuning knobs (capi.hip mx_llm_set_option; unknown keys and out-of-range values fail with
  * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
- * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max",
+ * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max", "rows_nt1",
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
  * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline), "engine_dbg" (timing

@@ -136,6 +136,8 @@ struct mx_llm {
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
+  int rows_nt1 = 11;                 // option: kinds whose 17-32-row launches take 16-row batch
+                                     // tiles (bit 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
   int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
                                      // (2: -22 us at 32 bf16 rows, -28 us at 8 e4m3 rows)
@@ -626,6 +628,16 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.tickets_n = x->rows_tickets_n;
 }
 
+// option rows_nt1: this kind's 17-32-row launch in two 16-row batch tiles instead of one
+// 32-row tile: twice the blocks (every CU streams; two 8-wave blocks fit a CU at 128 VGPRs),
+// each batch tile reading the weights once more (the two tiles' blocks run together, so the
+// second read is served on-die in part).  Measured at 20-32 rows, L 300 / 900: qkv + o-proj +
+// down (mask 11, the default) 4-5 % per step; gate/up and the lm_head lose
+// (profiles/r05_rows_nt1.log)
+static void nt_cap(const mx_llm* x, GemvArgs& g, int kind_bit, int R) {
+  if ((x->rows_nt1 >> kind_bit) & 1 && R <= 32) g.rows_nt_max = 1;
+}
+
 // Optional per-launch timing (eager runs only): prof->ev[k] brackets launch class k.
 enum { PK_QKV = 0, PK_ATTN, PK_O, PK_GU, PK_DOWN, PK_HEAD, PK_COMMIT, PK_ENGINE, PK_N };
 struct Prof {
@@ -653,6 +665,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     uint16_t* vc = x->vcache + x->kv_layer_elems * li;
     GemvArgs g{};
     attach_ws(x, g);
+    nt_cap(x, g, 0, rs.R);
     g.R = rs.R;
     g.eps = c.eps;
     // QKV + RoPE + KV append
@@ -676,6 +689,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // at one row, and at 2-16 rows when its tiling allows (option rows_merge)
     GemvArgs o{};
     attach_ws(x, o);
+    nt_cap(x, o, 1, rs.R);
     o.R = rs.R; o.W = l.wo; o.wscale = l.so; o.wdtype = c.wdtype; o.N = H; o.K = QD; o.X = x->att; o.xstride = QD; o.Y = rs.h;
     o.ystride = H; o.force_legacy = x->legacy_gemv; o.wpb = x->gemv_wpb; o.rpw = x->rpw_o;
     if (x->rows_frag) o.Wf = l.wo_f;
@@ -703,6 +717,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // gate/up + SiLU*up
     GemvArgs gu{};
     attach_ws(x, gu);
+    nt_cap(x, gu, 2, rs.R);
     gu.R = rs.R; gu.eps = c.eps; gu.W = l.wgu; gu.wscale = l.sgu; gu.wdtype = c.wdtype; gu.N = 2 * c.ffn; gu.K = H; gu.X = rs.h;
     gu.xstride = H; gu.norm_w = l.mlp_norm; gu.Y = x->act; gu.force_legacy = x->legacy_gemv; gu.wpb = x->gemv_wpb; gu.rpw = x->rpw_gu;
     if (x->rows_frag) gu.Wf = l.wgu_f;
@@ -713,6 +728,7 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     // down + residual
     GemvArgs d{};
     attach_ws(x, d);
+    nt_cap(x, d, 3, rs.R);
     d.R = rs.R; d.W = l.wd; d.wscale = l.sd; d.wdtype = c.wdtype; d.N = H; d.K = c.ffn; d.X = x->act; d.xstride = c.ffn; d.Y = rs.h;
     d.ystride = H; d.force_legacy = x->legacy_gemv; d.wpb = x->gemv_wpb; d.rpw = x->rpw_down;
     if (x->rows_frag) d.Wf = l.wd_f;
@@ -733,6 +749,7 @@ static hipError_t enqueue_head(mx_llm* x, const float* h, const int32_t* slot,
   float* lg = x->logits + (size_t)(best - x->best) * c.vocab;
   GemvArgs g{};
   attach_ws(x, g);
+  nt_cap(x, g, 4, R);
   g.R = R; g.eps = c.eps; g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype; g.N = c.vocab; g.K = c.hidden; g.X = h;
   g.xstride = c.hidden; g.norm_w = x->norm; g.row_slot = slot; g.seen = x->seen;
   g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = best;
@@ -1330,6 +1347,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_pw" || k == "rows_pw_f8") {
     if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw / rows_pw_f8 must be 1 or 2");
     (k == "rows_pw" ? x->rows_pw : x->rows_pw_f8) = value;
+  } else if (k == "rows_nt1") {
+    if (value < 0 || value > 31) MX_FAIL(x, MX_ERR_ARG, "rows_nt1 must be a 5-bit kind mask");
+    x->rows_nt1 = value;
   } else if (k == "rows_nt_max") {
     if (value != 0 && value != 1 && value != 2 && value != 4) MX_FAIL(x, MX_ERR_ARG, "rows_nt_max must be 0, 1, 2 or 4");
     x->rows_nt_max = value;

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
-            "rows_head_mt": 1, "rows_head_target": 0, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
+            "rows_head_mt": 1, "rows_head_target": 0, "rows_nt_max": 0, "rows_nt1": 11, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0}
 VARIANTS = {
     "base": {},
     "ticket": {"o_merge": 0, "att_cpw": 1},
@@ -39,6 +39,14 @@ VARIANTS = {
     "nw8": {"att_cpw": 1, "att_nw": 8},
     "hmt1": {"rows_head_mt": 1},
     "hmt2": {"rows_head_mt": 2},
+    "nt1_none": {"rows_nt1": 0},
+    "nt1_o": {"rows_nt1": 2},
+    "nt1_oq": {"rows_nt1": 3},
+    "nt1_od": {"rows_nt1": 10},
+    "nt1_oqd": {"rows_nt1": 11},
+    "nt1_ogu": {"rows_nt1": 6},
+    "nt1_oh": {"rows_nt1": 18},
+    "nt1_all": {"rows_nt1": 15},
     "nohead1": {"head_b1": 0},
     "tmerge": {"rows_merge": 0},
     "nwb4": {"att_nw_batch": 4},

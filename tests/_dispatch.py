@@ -45,7 +45,7 @@ FP8_SMALL = Dims(1024, 8, 2, 2048, 1000)
 # library option defaults (capi.hip struct mx_llm)
 DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
-                rows_nt_max=0, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
+                rows_nt_max=0, rows_nt1=11, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
                 rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7)
 
 
@@ -126,9 +126,17 @@ def _rows_key(MT, NT, epi, norm, sub, f8, o, nsm=0):
     return f"v4::gemm_rows_kernel<{MT}, {NT}, {epi}, {_b(norm)}, {sub}, {_b(f8)}, {pw}, {nsm}>"
 
 
-def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0):
+def nt_max_of(o, kind, R):
+    """capi.hip nt_cap: option rows_nt1 puts this kind's 17-32-row launches on 16-row tiles
+    (kind: 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head; None: not a layer launch)."""
+    if kind is not None and (o["rows_nt1"] >> kind) & 1 and R <= 32:
+        return 1
+    return o["rows_nt_max"]
+
+
+def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0, kind=None):
     """launch_gemm_rows_v4 -> the instantiation (None where it returns NotSupported)."""
-    mt, nt = rows_tiles(R, o["rows_nt_max"])
+    mt, nt = rows_tiles(R, nt_max_of(o, kind, R))
     if epi == EPI_ARGMAX and norm and o["rows_head_mt"] == 2 and nt in (1, 2):
         mt = 2
     if K % 128:
@@ -144,7 +152,7 @@ def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0):
 
 
 def rows_merge_ok(d, R, nsplit, o):
-    mt, nt = rows_tiles(R, o["rows_nt_max"])
+    mt, nt = rows_tiles(R, nt_max_of(o, 1, R))
     K = d.heads * 128
     if R < 2 or nt != 1 or K % 128 or nsplit < 1 or nsplit > 4:
         return False
@@ -171,7 +179,7 @@ def gemv1_launch(N, K, epi, norm, f8, o, rpw=0, nsm=0):
     return f"gemv1_kernel<{kch}, {rpw}, {epi}, {_b(norm)}, {o['gemv_wpb']}, {_b(f8)}, 0>"
 
 
-def gemv_launch(N, K, R, epi, norm, f8, o, rpw=0, nsm=0):
+def gemv_launch(N, K, R, epi, norm, f8, o, rpw=0, nsm=0, kind=None):
     """launch_gemv: the kernel one projection / lm_head launch runs."""
     if R == 1 and epi != EPI_ARGMAX and not o["legacy_gemv"]:
         k = gemv1_launch(N, K, epi, norm, f8, o, rpw, nsm)
@@ -183,7 +191,7 @@ def gemv_launch(N, K, R, epi, norm, f8, o, rpw=0, nsm=0):
     if R == 1 and epi == EPI_ARGMAX and norm and f8 and K % 1024 == 0:
         return "gemv_kernel<1, 8, 4, true, true>"
     if (R >= 2 and not o["legacy_gemv"]) or f8:
-        k = rows_launch(N, K, R, epi, norm, f8, o)
+        k = rows_launch(N, K, R, epi, norm, f8, o, kind=kind)
         if k or f8:
             return k
     rt = 1 if R == 1 else 4
@@ -208,7 +216,7 @@ def forward_keys(d, R, max_len, f8, opts=None, head_rows=None, sample=False):
         keys.add(f"eng::engine_kernel<{_b(f8)}, {d.grp}>")
         keys.add(gemv_launch(d.vocab, H, 1, EPI_ARGMAX, True, f8, o))
         return keys
-    keys.add(gemv_launch(QD + 2 * d.kv_heads * 128, H, R, EPI_QKV, True, f8, o))
+    keys.add(gemv_launch(QD + 2 * d.kv_heads * 128, H, R, EPI_QKV, True, f8, o, kind=0))
     nw, cpw, nsplit = att_shape(d, R, max_len, o)
     keys.add(f"attn_kernel<{d.grp}, {cpw}, {nw}>" + (PREFILL_TAG if head_rows == 1 and R > 1 else ""))
     b1_merge = R == 1 and not o["legacy_gemv"] and o["o_merge"] and nsplit <= 8
@@ -218,13 +226,13 @@ def forward_keys(d, R, max_len, f8, opts=None, head_rows=None, sample=False):
         keys.add(gemv_launch(H, QD, 1, EPI_RESID, False, f8, o,
                              rpw=o["rpw_o"] or 2, nsm=nsplit))
     elif rmerge:
-        keys.add(rows_launch(H, QD, R, EPI_RESID, False, f8, o, merge_nsm=nsplit))
+        keys.add(rows_launch(H, QD, R, EPI_RESID, False, f8, o, merge_nsm=nsplit, kind=1))
     else:
-        keys.add(gemv_launch(H, QD, R, EPI_RESID, False, f8, o, rpw=o["rpw_o"]))
-    keys.add(gemv_launch(2 * d.ffn, H, R, EPI_SILU, True, f8, o, rpw=o["rpw_gu"]))
-    keys.add(gemv_launch(H, d.ffn, R, EPI_RESID, False, f8, o, rpw=o["rpw_down"]))
+        keys.add(gemv_launch(H, QD, R, EPI_RESID, False, f8, o, rpw=o["rpw_o"], kind=1))
+    keys.add(gemv_launch(2 * d.ffn, H, R, EPI_SILU, True, f8, o, rpw=o["rpw_gu"], kind=2))
+    keys.add(gemv_launch(H, d.ffn, R, EPI_RESID, False, f8, o, rpw=o["rpw_down"], kind=3))
     hr = R if head_rows is None else head_rows
-    keys.add(gemv_launch(d.vocab, H, hr, EPI_ARGMAX, True, f8, o))
+    keys.add(gemv_launch(d.vocab, H, hr, EPI_ARGMAX, True, f8, o, kind=4))
     if sample:
         keys.add("sample_kernel")
     if None in keys:
