@@ -51,6 +51,8 @@ VARIANTS = {
     "tmerge": {"rows_merge": 0},
     "nwb4": {"att_nw_batch": 4},
     "cpwb2": {"att_cpw_batch": 2},
+    "cpwb4": {"att_cpw_batch": 4},
+    "cpwb6": {"att_cpw_batch": 6},
     "ht1024": {"rows_head_target": 1024},
     "ht2048": {"rows_head_target": 2048},
     "ht4096": {"rows_head_target": 4096},
