@@ -1084,8 +1084,9 @@ hipError_t launch_scatter_rows(void* dst, const void* src, const int32_t* dmap, 
   return hipGetLastError();
 }
 
-// Fragment-major copy of an [N][K] weight matrix for the multi-row GEMM: 16-row tiles, then
-// 128-k sub-chunks, then the WL = 2 esz load instructions of a sub-chunk, then the 64 lanes;
+// Fragment-major copy of an [N][K] weight matrix for the multi-row GEMM: 128-k sub-chunks, then
+// 16-row tiles (bf16; e4m3: tiles, then sub-chunks), then the WL = 2 esz load instructions of
+// a sub-chunk, then the 64 lanes;
 // lane (c, g) of instruction l holds row 16 t + c, bytes 16 (4 l + g) of the sub-chunk (the
 // same values the row-major addressing gives that lane).  Rows past N repeat row N - 1.
 __global__ void frag_major_kernel(const uint4* src, uint4* dst, int N, int K, int esz) {
@@ -1097,8 +1098,10 @@ __global__ void frag_major_kernel(const uint4* src, uint4* dst, int N, int K, in
   const int64_t q = u >> 6;  // instruction index
   const int l = (int)(q % WL);
   const int64_t ts = q / WL;
-  const int s = (int)(ts % S);
-  const int64_t t = ts / S;
+  // bf16: [sub-chunk][tile] order; e4m3: [tile][sub-chunk] (mx_rows_v4.inc wbase)
+  const int64_t T = (N + 15) / 16;
+  const int64_t t = esz == 2 ? ts % T : ts / S;
+  const int s = (int)(esz == 2 ? ts / T : ts % S);
   const int row = (int)min<int64_t>(16 * t + (lane & 15), N - 1);
   const int64_t row_units = (int64_t)K * esz / 16;
   dst[u] = src[(int64_t)row * row_units + (int64_t)s * (8 * esz) + 4 * l + (lane >> 4)];
