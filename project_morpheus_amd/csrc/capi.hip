@@ -1016,6 +1016,49 @@ extern "C" int mx_llm_bench_attention(mx_llm* x, int L, int n_rows, int cpw, int
   return MX_OK;
 }
 
+// The GEMV probes' launch arguments: layer li's projection `which` exactly as the decode step
+// sets it up (weights, fragment-major copies for the multi-row kernel, epilogue operands);
+// 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 the one-row merging o-proj, 5 lm_head.
+static GemvArgs bench_args(mx_llm* x, int which, int li, int n_rows, int merge_pos) {
+  const auto& c = x->c;
+  const int H = c.hidden, QD = c.heads * 128;
+  const LayerW& l = x->L[li];
+  GemvArgs g{};
+  attach_ws(x, g);
+  g.R = n_rows; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
+  g.wdtype = c.wdtype;
+  if (which == 0) {
+    g.W = l.wqkv; g.Wf = x->rows_frag ? l.wqkv_f : nullptr; g.wscale = l.sqkv;
+    g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
+    g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = x->row_slot;
+    g.row_pos = x->row_pos; g.kcache = x->kcache + x->kv_layer_elems * li;
+    g.vcache = x->vcache + x->kv_layer_elems * li; g.heads = c.heads; g.kv_heads = c.kv_heads;
+    g.max_pos = c.max_pos; g.Q = x->q;
+  } else if (which == 1) {
+    g.W = l.wo; g.Wf = x->rows_frag ? l.wo_f : nullptr; g.wscale = l.so; g.N = H; g.K = QD;
+    g.X = x->att; g.Y = x->act; g.rpw = x->rpw_o;
+  } else if (which == 2) {
+    g.W = l.wgu; g.Wf = x->rows_frag ? l.wgu_f : nullptr; g.wscale = l.sgu; g.N = 2 * c.ffn;
+    g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act; g.rpw = x->rpw_gu;
+  } else if (which == 3) {
+    g.W = l.wd; g.Wf = x->rows_frag ? l.wd_f : nullptr; g.wscale = l.sd; g.N = H; g.K = c.ffn;
+    g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
+  } else if (which == 4) {
+    g.W = l.wo; g.wscale = l.so; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act;
+    g.rpw = x->rpw_o > 0 ? x->rpw_o : 2;
+    g.att_ml = x->part_ml; g.att_acc = x->part_acc; g.att_S = 128;
+    g.att_stride = c.max_pos / ATT_S_MIN; g.att_nsm = (merge_pos + 128) / 128;
+    g.heads = c.heads; g.kv_heads = c.kv_heads; g.row_pos = x->row_pos;
+  } else {  // 5: lm_head + penalty + argmax (the same matrix every launch: 964 MB > MALL)
+    g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm;
+    g.N = c.vocab; g.K = H; g.X = x->h_dec; g.norm_w = x->norm; g.row_slot = x->row_slot;
+    g.seen = x->seen; g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = x->best;
+    g.logits = x->logits; g.logits_all = x->logits_all;
+  }
+  g.xstride = g.K; g.ystride = g.N;
+  return g;
+}
+
 // Roofline probe: one hipGraph of `reps` sweeps over all layers' GEMV `which` (0 qkv,
 // 1 o-proj, 2 gate/up, 3 down) for a single row, exactly as the decode step launches them
 // (same kernels, grids and epilogues; decode row 0's state is used and clobbered: the
@@ -1028,7 +1071,6 @@ static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
   if (n_rows < 1 || n_rows > c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows");
-  const int H = c.hidden, QD = c.heads * 128;
   MX_TRY(x, hipSetDevice(x->device));
   hipStream_t st = x->cap;
   if (which == 4 && n_rows != 1) MX_FAIL(x, MX_ERR_ARG, "the merging o-proj is one-row");
@@ -1042,39 +1084,7 @@ static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us
     MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
     MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
   }
-  auto args = [&](int li) {
-    const LayerW& l = x->L[li];
-    GemvArgs g{};
-    attach_ws(x, g);
-    g.R = n_rows; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
-    if (which == 0) {
-      g.W = l.wqkv; g.wscale = l.sqkv; g.wdtype = c.wdtype; g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
-      g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = x->row_slot;
-      g.row_pos = x->row_pos; g.kcache = x->kcache + x->kv_layer_elems * li;
-      g.vcache = x->vcache + x->kv_layer_elems * li; g.heads = c.heads; g.kv_heads = c.kv_heads;
-      g.max_pos = c.max_pos; g.Q = x->q;
-    } else if (which == 1) {
-      g.W = l.wo; g.wscale = l.so; g.wdtype = c.wdtype; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act; g.rpw = x->rpw_o;
-    } else if (which == 2) {
-      g.W = l.wgu; g.wscale = l.sgu; g.wdtype = c.wdtype; g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
-      g.rpw = x->rpw_gu;
-    } else if (which == 3) {
-      g.W = l.wd; g.wscale = l.sd; g.wdtype = c.wdtype; g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->q; g.rpw = x->rpw_down;
-    } else if (which == 4) {
-      g.W = l.wo; g.wscale = l.so; g.wdtype = c.wdtype; g.N = H; g.K = QD; g.X = x->att; g.Y = x->act;
-      g.rpw = x->rpw_o > 0 ? x->rpw_o : 2;
-      g.att_ml = x->part_ml; g.att_acc = x->part_acc; g.att_S = 128;
-      g.att_stride = c.max_pos / ATT_S_MIN; g.att_nsm = (merge_pos + 128) / 128;
-      g.heads = c.heads; g.kv_heads = c.kv_heads; g.row_pos = x->row_pos;
-    } else {  // 5: lm_head + penalty + argmax (the same matrix every launch: 964 MB > MALL)
-      g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype;
-      g.N = c.vocab; g.K = H; g.X = x->h_dec; g.norm_w = x->norm; g.row_slot = x->row_slot;
-      g.seen = x->seen; g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = x->best;
-      g.logits = x->logits; g.logits_all = x->logits_all;
-    }
-    g.xstride = g.K; g.ystride = g.N;
-    return g;
-  };
+  auto args = [&](int li) { return bench_args(x, which, li, n_rows, merge_pos); };
   const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : which == 5 ? EPI_ARGMAX : EPI_RESID;
   const bool norm = which == 0 || which == 2 || which == 5;
   MX_TRY(x, launch_gemv(args(0), epi, norm, st));
@@ -1132,7 +1142,6 @@ extern "C" int mx_llm_bench_gemv_streams(mx_llm* x, int which, int n_rows, int r
   const auto& c = x->c;
   if (n_rows < 2 || n_rows > c.max_batch) MX_FAIL(x, MX_ERR_ARG, "bad n_rows (multi-row only)");
   MX_TRY(x, hipSetDevice(x->device));
-  const int H = c.hidden, QD = c.heads * 128;
   {
     std::vector<int32_t> slots(n_rows), pos(n_rows, 0);
     for (int i = 0; i < n_rows; ++i) slots[i] = i % c.max_slots;
@@ -1155,33 +1164,9 @@ extern "C" int mx_llm_bench_gemv_streams(mx_llm* x, int which, int n_rows, int r
     if (e == hipSuccess) e = hipEventCreate(&done[s]);
   }
   auto args = [&](int li, int s) {
-    const LayerW& l = x->L[li];
-    GemvArgs g{};
-    attach_ws(x, g);
+    GemvArgs g = bench_args(x, which, li, n_rows, 0);
     g.ws = ws[s];
     g.tickets = tk[s];
-    g.R = n_rows; g.eps = c.eps; g.wpb = x->gemv_wpb; g.force_legacy = x->legacy_gemv;
-    g.row_slot = x->row_slot; g.row_pos = x->row_pos;
-    if (which == 0) {
-      g.W = l.wqkv; g.Wf = x->rows_frag ? l.wqkv_f : nullptr; g.wscale = l.sqkv; g.wdtype = c.wdtype;
-      g.N = QD + 2 * c.kv_heads * 128; g.K = H; g.X = x->h_dec; g.norm_w = l.attn_norm;
-      g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.kcache = x->kcache; g.vcache = x->vcache;
-      g.heads = c.heads; g.kv_heads = c.kv_heads; g.max_pos = c.max_pos; g.Q = x->q;
-    } else if (which == 1) {
-      g.W = l.wo; g.Wf = x->rows_frag ? l.wo_f : nullptr; g.wscale = l.so; g.wdtype = c.wdtype;
-      g.N = H; g.K = QD; g.X = x->att; g.Y = x->h_dec;
-    } else if (which == 2) {
-      g.W = l.wgu; g.Wf = x->rows_frag ? l.wgu_f : nullptr; g.wscale = l.sgu; g.wdtype = c.wdtype;
-      g.N = 2 * c.ffn; g.K = H; g.X = x->h_dec; g.norm_w = l.mlp_norm; g.Y = x->act;
-    } else if (which == 3) {
-      g.W = l.wd; g.Wf = x->rows_frag ? l.wd_f : nullptr; g.wscale = l.sd; g.wdtype = c.wdtype;
-      g.N = H; g.K = c.ffn; g.X = x->act; g.Y = x->h_dec;
-    } else {
-      g.W = x->lm; g.Wf = x->rows_frag ? x->lm_f : nullptr; g.wscale = x->slm; g.wdtype = c.wdtype;
-      g.N = c.vocab; g.K = H; g.X = x->h_dec; g.norm_w = x->norm;
-      g.seen = x->seen; g.penalty = x->penalty; g.samp_temp = x->samp_temp; g.best = x->best;
-    }
-    g.xstride = g.K; g.ystride = g.N;
     return g;
   };
   const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : which == 5 ? EPI_ARGMAX : EPI_RESID;
