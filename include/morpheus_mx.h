@@ -94,6 +94,12 @@ int mx_llm_prefill(mx_llm* ctx, int slot, int row, const int32_t* ids_host, int 
 /* One decode step for rows [0, n_rows), each under its slot's parameters (hipGraph-captured
  * per row count and attention grid; replayed). */
 int mx_llm_decode(mx_llm* ctx, int n_rows, void* stream);
+/* After the host has waited for a step: MX_ERR_HIP if a persistent-engine launch (option
+ * b1_engine) gave up on a bounded wait since the last check.  Such a step commits nothing (its
+ * history entry reads -1, the row does not advance); this call waits for `stream`, clears the
+ * engine's attention tickets and re-reads the row positions, so the next mx_llm_decode
+ * recomputes the step.  mx_llm_decode performs the same check before it enqueues. */
+int mx_llm_check(mx_llm* ctx, void* stream);
 /* Same step launched eagerly (no graph) with HIP events around every launch; adds the
  * elapsed milliseconds per launch class to ms_by_class[k] (k < n_classes; classes:
  * 0 qkv, 1 attention, 2 o-proj, 3 gate/up, 4 down, 5 lm_head+argmax, 6 commit, 7 the
@@ -105,9 +111,11 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max", "rows_nt1",
- * "rows_pw", "rows_pw_f8", "rows_lds_pad", "b1_engine" (one-row steps as ONE persistent
+ * "rows_pw", "rows_pw_f8", "rows_lds_pad", "rows_atomic" (o-proj / down at >= 2 rows: K ranges
+ * add into the residual with float atomics, no split-K seam), "b1_engine" (one-row steps as ONE persistent
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
- * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline), "engine_dbg" (timing
+ * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline),
+ * "engine_timeout" (bound of every engine wait, 100 MHz ticks; 0 = 50 ms), "engine_dbg" (timing
  * experiments: 1 = no hand-off waits, 2 = no weight stream; outputs invalid).  Drops
  * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);

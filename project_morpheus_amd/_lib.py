@@ -62,6 +62,7 @@ _SIGS = {
     "mx_llm_finalize": (C.c_int, [_P]),
     "mx_llm_prefill": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int, C.POINTER(Sampling), _P]),
     "mx_llm_decode": (C.c_int, [_P, C.c_int, _P]),
+    "mx_llm_check": (C.c_int, [_P, _P]),
     "mx_llm_decode_profiled": (C.c_int, [_P, C.c_int, _P, C.POINTER(C.c_double), C.c_int]),
     "mx_llm_set_option": (C.c_int, [_P, C.c_char_p, C.c_int]),
     "mx_llm_engine_trace": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_int)]),
@@ -109,7 +110,12 @@ def load(path: str = LIB_PATH):
             lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
         except OSError as e:
             raise MxUnavailable(f"cannot load {path}: {e}") from e
+        # an older library named by MORPHEUS_MX_LIB (same-box A/B runs) may lack entry points
+        # added since; the in-tree product library must export every one
+        older = os.path.abspath(path) != os.path.join(HERE, "libmorpheus_mx.so")
         for name, (res, args) in _SIGS.items():
+            if older and not hasattr(lib, name):
+                continue
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args

@@ -525,6 +525,7 @@ class BatchSynthesizer:
                 continue
             ev, entries = inflight.popleft()
             ev.synchronize()
+            llm.check(self.stream)
             due: List = []
             for r, req, k in entries:
                 if r.req is not req or r.stopped or req.cancelled:

@@ -140,7 +140,13 @@ struct mx_llm {
                                      // tiles (bit 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
   int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
-                                     // (2: -22 us at 32 bf16 rows, -28 us at 8 e4m3 rows)
+                                     // (1 since round 5: with one argmax atomic per block the
+                                     // 128-VGPR 16-row tiles stream faster: 8 bf16 rows 172.6
+                                     // -> 149.7 us, 8 e4m3 rows -> 79.6 us, 32 rows -> 154 us;
+                                     // profiles/r05_head_options.log)
+  int rows_atomic = 1;               // option: residual projections (o-proj, down) at >= 2 rows
+                                     // add each K range's partial into h with float atomics
+                                     // instead of the split-K seam (mx_rows_v4.inc)
   int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
@@ -148,6 +154,8 @@ struct mx_llm {
   // one-row decode step as one launch (engine_slots = its LDS ring depth)
   int b1_engine = 0, engine_slots = 7, engine_depth = 2, engine_loaders = 2, engine_grid = 0;
   int engine_dbg = 0;  // option engine_dbg: timing experiments (outputs invalid when != 0)
+  int engine_timeout_ticks = 5000000;  // option engine_timeout: bound of every engine wait in
+                                       // 100 MHz ticks (50 ms; a step takes ~1.5 ms)
   uint2 *g_qkv = nullptr, *g_att = nullptr, *g_h1 = nullptr, *g_act = nullptr, *g_h2 = nullptr;
   float* eng_part = nullptr;
   int* eng_tickets = nullptr;
@@ -621,6 +629,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_nt_max = x->rows_nt_max;
   g.rows_head_target = x->rows_head_target;
   g.rows_head_mt = x->rows_head_mt;
+  g.rows_atomic = x->rows_atomic;
   g.head_b1 = x->head_b1;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -798,7 +807,7 @@ static EngineArgs engine_args(const mx_llm* x) {
   a.max_pos = c.max_pos; a.smax = (c.max_pos + 127) / 128; a.ring_slots = x->engine_slots;
   a.f8 = c.wdtype == WT_FP8 ? 1 : 0; a.eps = c.eps; a.depth = x->engine_depth; a.loaders = x->engine_loaders;
   a.xb = engine_xb_floats(c.heads, c.kv_heads, c.ffn);
-  a.timeout_ticks = 5000000;  // 50 ms of the 100 MHz clock (a step takes ~1.5 ms)
+  a.timeout_ticks = x->engine_timeout_ticks;
   a.trace = x->eng_trace;
   a.dbg = x->engine_dbg;
   return a;
@@ -830,6 +839,8 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, bo
     cm.row_token = x->row_token; cm.seen = x->seen; cm.hist = x->hist_dev; cm.embed = x->embed;
     cm.h = x->h_dec; cm.hidden = c.hidden; cm.vocab = c.vocab; cm.max_pos = c.max_pos;
     cm.pos_advance = 1; cm.scratch_slot = c.max_slots;
+    // an engine launch that gave up commits nothing (its history entry reads -1)
+    cm.abort_word = (n_rows == 1 && x->b1_engine) ? x->eng_status_d : nullptr;
     e = launch_commit(cm, n_rows, st);
   }
   PROF_END();
@@ -885,6 +896,32 @@ static void mirror_step(mx_llm* x, int n_rows) {
     if (x->row_active[r]) x->pos_mirror[r] = std::min(x->pos_mirror[r] + 1, x->c.max_pos - 1);
 }
 
+// A persistent-engine launch that gave up (a bounded wait expired) leaves its status word set.
+// Its attention tickets may be non-zero (a split that arrived before the abort), and the next
+// launch would then take `t == S - 1` early and merge stale partials: wait for the stream, clear
+// the tickets (the epoch finish counter is consistent -- every workgroup counts itself out, abort
+// or not), clear the word, report.  Returns 1 (x->err set) when it gave up.
+static int engine_gave_up(mx_llm* x, hipStream_t st) {
+  if (!x->eng_status_h || !__atomic_load_n(x->eng_status_h, __ATOMIC_ACQUIRE)) return 0;
+  (void)hipStreamSynchronize(st);
+  (void)hipDeviceSynchronize();
+  (void)hipMemset(x->eng_tickets, 0, (size_t)x->c.layers * x->c.kv_heads * 4);
+  // the steps that did not commit did not advance their rows: re-read the positions
+  std::vector<int32_t> pos(x->c.max_batch, 0);
+  if (hipMemcpy(pos.data(), x->row_pos, pos.size() * 4, hipMemcpyDeviceToHost) == hipSuccess)
+    for (int r = 0; r < x->c.max_batch; ++r)
+      if (x->row_active[r]) x->pos_mirror[r] = pos[r];
+  const int s = __atomic_exchange_n(x->eng_status_h, 0, __ATOMIC_ACQ_REL);
+  x->err = "persistent engine launch gave up (status " + std::to_string(s) +
+           "): a hand-off timed out; that step's token was not committed";
+  return 1;
+}
+
+extern "C" int mx_llm_check(mx_llm* x, void* stream) {
+  if (!x) return MX_ERR_ARG;
+  return engine_gave_up(x, (hipStream_t)stream) ? MX_ERR_HIP : MX_OK;
+}
+
 static int check_room(mx_llm* x, int n_rows) {
   for (int r = 0; r < n_rows; ++r)
     if (x->row_active[r] && x->pos_mirror[r] >= x->c.max_pos - 1)
@@ -899,11 +936,7 @@ extern "C" int mx_llm_decode(mx_llm* x, int n_rows, void* stream) {
   if (check_room(x, n_rows)) return MX_ERR_STATE;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(x, hipSetDevice(x->device));
-  if (x->eng_status_h && __atomic_load_n(x->eng_status_h, __ATOMIC_ACQUIRE)) {
-    const int s = __atomic_exchange_n(x->eng_status_h, 0, __ATOMIC_ACQ_REL);
-    MX_FAIL(x, MX_ERR_HIP, "persistent engine launch gave up (status " + std::to_string(s) +
-                               "): a hand-off timed out; the step's outputs are invalid");
-  }
+  if (engine_gave_up(x, st)) return MX_ERR_HIP;
   // one graph per (row count, attention split count): kernels read positions from device
   // memory; the split count only sizes the attention grid (the engine sizes its own)
   const bool engine = n_rows == 1 && x->b1_engine;
@@ -1056,6 +1089,9 @@ static GemvArgs bench_args(mx_llm* x, int which, int li, int n_rows, int merge_p
     g.logits = x->logits; g.logits_all = x->logits_all;
   }
   g.xstride = g.K; g.ystride = g.N;
+  // the step's batch-tile choice (option rows_nt1) for this kind: 0-3 as listed, 4 is the
+  // one-row o-proj (kind bit 1), 5 the lm_head (kind bit 4)
+  nt_cap(x, g, which == 5 ? 4 : which == 4 ? 1 : which, n_rows);
   return g;
 }
 
@@ -1066,7 +1102,7 @@ static GemvArgs bench_args(mx_llm* x, int which, int li, int n_rows, int merge_p
 // out of the 256 MB Infinity Cache, as in a real step.  Writes mean microseconds per
 // launch (inter-kernel gap in the graph included) and the weight bytes of one launch.
 static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us_out,
-                           double* bytes_out, unsigned long long* trace) {
+                           double* bytes_out, unsigned long long* trace, int trace_cap = 0) {
   if (!x || !us_out || which < 0 || which > 5 || reps < 1) return MX_ERR_ARG;
   if (!x->final) MX_FAIL(x, MX_ERR_STATE, "not finalized");
   const auto& c = x->c;
@@ -1096,7 +1132,10 @@ static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us
   for (int i = 0; i < reps && e == hipSuccess; ++i)
     for (int li = 0; li < c.layers && e == hipSuccess; ++li) {
       GemvArgs g = args(li);
-      if (i == reps - 1 && li == c.layers - 1) g.trace = trace;  // the sweep's last launch
+      if (i == reps - 1 && li == c.layers - 1) {  // the sweep's last launch
+        g.trace = trace;
+        g.trace_cap = trace_cap;  // stamps of blocks past the buffer are dropped
+      }
       e = launch_gemv(g, epi, norm, st);
     }
   hipError_t e2 = hipStreamEndCapture(st, &g);
@@ -1226,7 +1265,7 @@ extern "C" int mx_llm_bench_gemv_trace(mx_llm* x, int which, int n_rows, uint64_
   MX_TRY(x, hipMalloc(&d, n * 8));
   hipError_t e = hipMemset(d, 0, n * 8);
   float us = 0.f;
-  int rc = e == hipSuccess ? bench_gemv_impl(x, which, n_rows, 1, &us, nullptr, d) : MX_ERR_HIP;
+  int rc = e == hipSuccess ? bench_gemv_impl(x, which, n_rows, 1, &us, nullptr, d, cap_blocks) : MX_ERR_HIP;
   if (rc == MX_OK) e = hipMemcpy(host_out, d, n * 8, hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (rc != MX_OK) return rc;
@@ -1263,9 +1302,10 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     const int depth = k == "engine_depth" ? value : x->engine_depth;
     if (k == "b1_engine" && value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "b1_engine must be 0 or 1");
     if (depth != 2 && depth != 3) MX_FAIL(x, MX_ERR_ARG, "engine_depth must be 2 or 3");
-    if (slots < 3 || slots > 8 || slots <= depth ||
+    if (slots < 3 || slots > engine_ring_max() || slots <= depth ||
         engine_lds_bytes(slots, x->c.hidden, engine_xb_floats(x->c.heads, x->c.kv_heads, x->c.ffn)) > 160 * 1024)
-      MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3..8, above engine_depth, and fit the CU's 160 KB of LDS");
+      MX_FAIL(x, MX_ERR_ARG, "engine_slots must be 3.." + std::to_string(engine_ring_max()) +
+                                 ", above engine_depth, and fit the CU's 160 KB of LDS");
     if (en) {
       const auto& c = x->c;
       MX_TRY(x, hipSetDevice(x->device));
@@ -1291,6 +1331,10 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     x->engine_slots = slots;
     x->engine_depth = depth;
     x->b1_engine = en ? 1 : 0;
+  } else if (k == "engine_timeout") {
+    // (tests force a give-up with a tiny bound; 0 restores the default)
+    if (value < 0) MX_FAIL(x, MX_ERR_ARG, "engine_timeout must be >= 0 (ticks of 100 MHz; 0 = 50 ms)");
+    x->engine_timeout_ticks = value ? value : 5000000;
   } else if (k == "engine_dbg") {
     if (value < 0 || value > 3) MX_FAIL(x, MX_ERR_ARG, "engine_dbg must be 0..3");
     x->engine_dbg = value;
@@ -1302,6 +1346,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
       MX_TRY(x, hipMemset(x->eng_trace, 0, (size_t)1024 * x->c.layers * 12 * 8));
     }
     if (!value) x->eng_trace = nullptr;  // (the buffer stays allocated until destroy)
+  } else if (k == "rows_atomic") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_atomic must be 0 or 1");
+    x->rows_atomic = value;
   } else if (k == "head_b1") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "head_b1 must be 0 or 1");
     x->head_b1 = value;

@@ -190,7 +190,7 @@ __device__ __forceinline__ bool cbar(Ctl* ctl, int& gen, const Clock& clk, int* 
   int spins = 0;
   while (lds_ld(&ctl->bar) < gen) {
     __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+    if ((spins++ & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
       lds_st(&ctl->abort_, 1);
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
@@ -238,7 +238,7 @@ __device__ __forceinline__ bool gather(const uint2* g, int n, uint32_t tag, floa
           ok[j] = v[j].y == tag && v[j].w == tag;
         }
       }
-      if ((++spins & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+      if ((spins++ & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
         lds_st(&ctl->abort_, 1);
         __hip_atomic_store(status, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return false;
@@ -379,7 +379,7 @@ __device__ __forceinline__ bool witness(const uint2* g, int n, int per, uint32_t
       const u32x4v v = gget2(g, wi & ~1);
       if ((wi & 1 ? v.w : v.y) == tag) break;
       __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+      if ((spins++ & 63) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
         lds_st(&ctl->abort_, 1);
         __hip_atomic_store(status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return false;
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(64 * (NC + NL), 1) void engine_kernel(EngineArgs a)
           publish_all();
           while (loader_ld(&ctl->freed[pos]) != k - NS + 1) {
             __builtin_amdgcn_s_sleep(2);
-            if ((++spins & 255) == 0 && (loader_ld(&ctl->abort_) || clk.expired())) {
+            if ((spins++ & 255) == 0 && (loader_ld(&ctl->abort_) || clk.expired())) {
               dead = true;
               return;
             }
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(64 * (NC + NL), 1) void engine_kernel(EngineArgs a)
       int spins = 0;
       while (ring_ld(&ctl->ready[pos]) != kk + 1) {
         __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
+        if ((spins++ & 255) == 0 && (lds_ld(&ctl->abort_) || clk.expired())) {
           lds_st(&ctl->abort_, 1);
           if (lane == 0) __hip_atomic_store(a.status, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           return nullptr;
@@ -981,6 +981,7 @@ int engine_xb_floats(int heads, int kv_heads, int F) {
   const int att = grp * 128 + 256 + (eng::NC + 1) * grp * 130;
   return std::max(std::max(F, heads * 128), att);
 }
+int engine_ring_max() { return eng::RING_MAX; }
 // the engine's LDS is static (eng::RING_MAX slots, XA_MAX / XB_MAX floats): shapes must fit it
 size_t engine_lds_bytes(int ring_slots, int H, int xb_floats) {
   if (ring_slots > eng::RING_MAX || H > eng::XA_MAX || xb_floats > eng::XB_MAX) return ~(size_t)0;
@@ -1010,9 +1011,14 @@ hipError_t engine_per_cu(const EngineArgs& a, int* per_cu) {
 
 hipError_t launch_engine_b1(const EngineArgs& a, int grid, hipStream_t st) {
   const size_t lds = engine_lds_bytes(a.ring_slots, a.H, a.xb);
-  if (a.ring_slots < 3 || a.ring_slots > 8 || a.ring_slots <= a.depth || lds > 160 * 1024 ||
-      a.layers > 31)
+  if (a.ring_slots < 3 || a.ring_slots > eng::RING_MAX || a.ring_slots <= a.depth ||
+      lds > 160 * 1024 || a.layers > 31)
     return hipErrorInvalidValue;
+  // Xb must hold the attention scratch: before 5129db2 it was sized by the ffn width alone, and
+  // on the small test shape (GQA 4, ffn 2,048 < 3,368 scratch floats) the attention items wrote
+  // past it into the control block (ring flags, barrier count), so a CU stopped publishing and
+  // its consumers' gathers timed out (status 3, gpurun_out/r05_eng1/tests.log).  Assert it here.
+  if (a.xb < engine_xb_floats(a.heads, a.kv_heads, a.F) || a.xb > eng::XB_MAX) return hipErrorInvalidValue;
   if (a.H % 1024 || a.F % 1024 || a.heads * 128 != a.H) return hipErrorNotSupported;
   const void* fn = engine_fn(a);
   if (!fn) return hipErrorNotSupported;

@@ -807,7 +807,14 @@ __global__ __launch_bounds__(256) void commit_kernel(CommitArgs a) {
     tok_s = tok;
     a.best[r] = 0ull;
     const int slot = a.row_slot[dst];
-    if (slot != a.scratch_slot) {  // parked rows stay at position 0 of the scratch slot
+    const bool gave_up = a.abort_word &&
+        __hip_atomic_load(a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    if (gave_up) {  // the step's outputs are invalid: no advance, the history slot reads -1,
+                    // and h is the step's input again (the engine overwrites it in place)
+      if (slot != a.scratch_slot)
+        a.hist[(size_t)slot * a.max_pos + min(a.row_pos[dst] + a.pos_advance, a.max_pos - 1)] = -1;
+      tok_s = a.row_token[dst];
+    } else if (slot != a.scratch_slot) {  // parked rows stay at position 0 of the scratch slot
       const int pos = min(a.row_pos[dst] + a.pos_advance, a.max_pos - 1);  // new token
       a.row_pos[dst] = pos;
       a.row_token[dst] = tok;

@@ -31,6 +31,7 @@ struct EngineArgs {
 };
 
 int engine_xb_floats(int heads, int kv_heads, int F);
+int engine_ring_max();  // ring slots the engine's static LDS holds
 size_t engine_lds_bytes(int ring_slots, int H, int xb_floats);
 // engine workgroups one CU holds (sets the kernel's dynamic-LDS limit; call outside capture)
 hipError_t engine_per_cu(const EngineArgs& a, int* per_cu);

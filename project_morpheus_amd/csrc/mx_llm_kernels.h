@@ -41,7 +41,10 @@ struct GemvArgs {
   int rows_nt_max;         // generation 4: largest batch tile in 16-row units (0 = 4)
   int rows_head_target;    // generation 4: K-range target of the lm_head (0 = the default 192)
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
+  int rows_atomic;         // generation 4, residual projections split over K: every K range
+                           // adds its partial tile into Y with float atomics (no seam)
   unsigned long long* trace;  // generation 4 diagnostic: [block][8] phase stamps (null = off)
+  int trace_cap;           // blocks the trace buffer holds (stamps of later blocks are dropped)
   int head_b1;             // R = 1 lm_head on the persistent kernel (head_b1.hip; 0 = gemv_kernel)
   // EPI_QKV
   const float* rope_cos;   // [max_pos][64]
@@ -97,6 +100,8 @@ struct CommitArgs {
   float* h;
   int hidden, vocab, max_pos, pos_advance;
   int scratch_slot;          // rows bound to this slot are parked: no advance, no history
+  const int* abort_word;     // null, or the persistent engine's host-mapped status: when set,
+                             // nothing is committed and the history entry reads -1
 };
 
 

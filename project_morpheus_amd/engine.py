@@ -96,6 +96,11 @@ class LlmEngine:
         """One step for rows [0, n_rows), each under its slot's generation parameters."""
         self._check(self.lib.mx_llm_decode(self.h, n_rows, C.c_void_p(stream.cuda_stream)))
 
+    def check(self, stream) -> None:
+        """After waiting for a step: raises if a persistent-engine launch gave up on a
+        bounded wait (that step committed nothing; the next decode recomputes it)."""
+        self._check(self.lib.mx_llm_check(self.h, C.c_void_p(stream.cuda_stream)))
+
     PROFILE_CLASSES = ("qkv", "attention", "o_proj", "gate_up", "down", "lm_head", "commit",
                        "engine")
 
@@ -377,6 +382,7 @@ class Synthesizer:
                     launched += 1
                 k, e = inflight.popleft()
                 e.synchronize()
+                llm.check(self.stream)
                 tok = int(llm.hist[slot, n0 + k])
                 done += 1
                 st.tokens += 1

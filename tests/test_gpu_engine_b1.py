@@ -127,3 +127,55 @@ def test_engine_status_word_stays_clear_over_many_steps():
     eng.decode(1, st)   # raises if any earlier launch timed out
     st.synchronize()
     eng.close()
+
+
+def test_engine_give_up_commits_nothing_and_recovers():
+    """A forced give-up (option engine_timeout = 1 tick) mid-stream: the failed steps commit
+    nothing (history -1, the row does not advance, h is the step's input again), the host check
+    raises and clears the attention tickets, and with the default bound restored the stream
+    continues exactly as the oracle's (L 251..280: 2 -> 3 splits, the ticket merge)."""
+    from oracle import llama_ref as L
+    from project_morpheus_amd._lib import MxError
+    from project_morpheus_amd.engine import LlmEngine
+
+    from _parity import check_tokens
+    cfg = _small()
+    w = synthetic_llm_weights(cfg, seed=105, std=0.05, norm_jitter=0.5)
+    prompt = [int(x) for x in np.random.default_rng(9).integers(0, cfg.vocab, 250)]
+    eng = LlmEngine(cfg, w, device=0, max_slots=1, max_pos=512, max_batch=1, max_prefill=256)
+    eng.set_option("b1_engine", 1)
+    eng.enable_logits()
+    st = torch.cuda.Stream()
+    toks, logits = [], []
+
+    def record(k):
+        st.synchronize()
+        eng.check(st)
+        logits.append(eng.read_logits(0, st))
+        toks.append(int(eng.hist[0, len(prompt) + k]))
+
+    eng.prefill(0, 0, prompt, 1.1, st)
+    record(0)
+    for k in range(1, 10):
+        eng.decode(1, st)
+        record(k)
+    eng.set_option("engine_timeout", 1)
+    eng.decode(1, st)
+    st.synchronize()
+    with pytest.raises(MxError, match="gave up"):
+        eng.check(st)
+    assert int(eng.hist[0, len(prompt) + 10]) == -1
+    eng.check(st)  # cleared
+    eng.set_option("engine_timeout", 0)
+    for k in range(10, 30):
+        eng.decode(1, st)
+        record(k)
+    eng.close()
+    rc = L.RefConfig(hidden=cfg.hidden, layers=cfg.layers, heads=cfg.heads,
+                     kv_heads=cfg.kv_heads, ffn=cfg.ffn, vocab=cfg.vocab)
+    ref = L.LlamaRef(rc, w, max_pos=512)
+    _, r_logits = L.greedy_generate(ref, prompt, len(toks), 1.1, return_logits=True, forced=toks)
+    for k in range(len(toks)):
+        np.testing.assert_allclose(logits[k], r_logits[k].numpy(), atol=5e-3, rtol=5e-3,
+                                   err_msg=f"step {k}")
+    assert check_tokens(toks, r_logits, 1e-2) >= 0.75 * len(toks)

@@ -416,6 +416,15 @@ def test_batched_decode_orpheus_width_6_rows():
     assert _compare_rows(cfg, w, _orpheus_prompts(6, 24, 6, 1), 6) >= 0.8 * 6 * 6
 
 
+def test_batched_decode_orpheus_width_6_rows_split_k_seam():
+    """Option rows_atomic = 0: the o-proj and down K ranges merged by the split-K seam
+    (write-through partials, ticket, last-arriver merge) instead of float atomics into h."""
+    cfg = _cfgs("orpheus2")
+    w = synthetic_llm_weights(cfg, seed=25)
+    assert _compare_rows(cfg, w, _orpheus_prompts(6, 26, 6, 1), 6,
+                         options={"rows_atomic": 0}) >= 0.8 * 6 * 6
+
+
 def test_batched_decode_orpheus_width_32_rows():
     """configs[2]'s shape: 32 rows at Orpheus widths (two 16-row batch tiles per weight tile,
     the kernels bench.py times for B = 32), ragged prompts."""
