@@ -124,7 +124,8 @@ def dry_run(args, rank: int, world: int) -> None:
         dist.destroy_process_group()
 
 
-PMC_RECORD = next((f for f in ("r04_pmc_gemv.json", "r03_pmc_gemv.json", "r02_pmc_gemv.json")
+PMC_RECORD = next((f for f in ("r06_pmc_gemv.json", "r04_pmc_gemv.json", "r03_pmc_gemv.json",
+                               "r02_pmc_gemv.json")
                    if os.path.exists(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                   "profiles", f))), "r02_pmc_gemv.json")
 
@@ -139,6 +140,38 @@ def pmc_traffic(kind, record=PMC_RECORD):
             return json.load(fh)["kernels"][kind]["traffic_bytes"]
     except (OSError, KeyError, ValueError):
         return None
+
+
+# the dominant kernel as rocprofv3 names it (so the line joins the committed kernel-trace
+# summaries under profiles/ mechanically)
+ROOFLINE_KERNEL = "gemv1_kernel<6, 2, 2, true, 4, false, 0>"
+
+
+def rocprof_fields(nbytes):
+    """The same kernel's frac from the committed rocprofv3 average (kernel time only)."""
+    us, path = rocprof_avg_us()
+    if us is None:
+        return {}
+    return {"rocprof_avg_us": round(us, 3), "rocprof_frac": round(nbytes / (us * 1e3) / PEAK_HBM_GBS, 4),
+            "rocprof_source": path}
+
+
+def rocprof_avg_us(kernel=ROOFLINE_KERNEL):
+    """(average launch duration in us, file) of ``kernel`` in the newest committed rocprofv3
+    --kernel-trace --stats summary of a whole bench run (profiles/r*_bench_kernel_stats*.csv)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats*.csv")),
+                   key=lambda f: (os.path.basename(f)[:3], os.path.getmtime(f)))
+    for path in reversed(files):
+        try:
+            with open(path) as fh:
+                for r in csv.DictReader(fh):
+                    if f"mx::{kernel}(" in r.get("Name", ""):
+                        return float(r["AverageNs"]) / 1e3, os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 from project_morpheus_amd.config import synthetic_audio_ids  # noqa: E402
@@ -704,10 +737,14 @@ def main():
             "decode_tok_per_s": round(1e3 / step_ms, 1),
             "step_roofline": {"bytes": step_bytes, "achieved_gbs": round(step_bytes / step_ms / 1e6, 1),
                               "frac": round(step_bytes / step_ms / 1e6 / PEAK_HBM_GBS, 4)},
-            "roofline": {"kernel": "gemv1_kernel<6,2,EPI_SILU,NORM,4> (RMSNorm + gate/up + SiLU*up)",
+            "roofline": {"kernel": ROOFLINE_KERNEL,
+                         "what": "one-row RMSNorm + gate/up [16384 x 3072] + SiLU*up (EPI_SILU, NORM)",
                          "bound": "hbm", "achieved": round(gu_gbs, 1), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(gu_gbs / PEAK_HBM_GBS, 4),
                          "avg_launch_us": round(gu_us, 3), "bytes_per_launch": gu_bytes,
+                         "avg_launch_us_source": "HIP events around one hipGraph of 4 x 28 "
+                                                 "back-to-back launches (launch gaps included)",
+                         **rocprof_fields(gu_bytes),
                          "traffic": pmc_traffic("gate_up"),
                          "traffic_source": f"profiles/{PMC_RECORD} (rocprofv3 --pmc "
                                            "FETCH_SIZE / WRITE_SIZE, separate passes)"},

@@ -11,4 +11,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   python3 scripts/pmc_summary.py $f > $OUT/$c.summary.json
   rm -f $f
 done
-python3 scripts/pmc_gemv_record.py $OUT/FETCH_SIZE.summary.json $OUT/WRITE_SIZE.summary.json $OUT/r04_pmc_gemv.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes, scripts/gpu_pmc_b1.sh) over scripts/pmc_gemv.py --rows 1: one graph sweep of all 28 layers per GEMV (no Infinity-Cache reuse), bf16; hbm_read_bytes = FETCH_SIZE x 1024 x 2 (gfx950 correction, MI355X_MICROARCH.md HBM), hbm_write_bytes = WRITE_SIZE x 1024; medians"
+python3 scripts/pmc_gemv_record.py $OUT/FETCH_SIZE.summary.json $OUT/WRITE_SIZE.summary.json $OUT/pmc_gemv.json "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes, scripts/gpu_pmc_b1.sh) over scripts/pmc_gemv.py --rows 1: one graph sweep of all 28 layers per GEMV (no Infinity-Cache reuse), bf16; hbm_read_bytes = FETCH_SIZE x 1024 x 2 (gfx950 correction, MI355X_MICROARCH.md HBM), hbm_write_bytes = WRITE_SIZE x 1024; medians"

@@ -109,6 +109,23 @@ GPU_RUNS = {
 }
 
 
+# SNAC: test node -> the (frames, windows) of each mx_snac_decode call it compares with the
+# oracle (tests/_snac_dispatch.py derives the kernel keys; tests/test_snac_coverage.py checks
+# them against the serving envelope and the bench trace)
+SNAC_RUNS = {
+    **{f"test_gpu_snac.py::test_snac_window_parity[{n}-{b}]": [(n, b)]
+       for n, b in ((1, 1), (4, 1), (7, 1), (7, 3), (2, 2), (1, 5), (4, 9), (7, 12))},
+    "test_gpu_snac.py::test_snac_batched_32_windows_matches_oracle": [(7, 32)],
+}
+
+
+def check_declared_snac(n_frames, batch):
+    node = current_test()
+    runs = SNAC_RUNS.get(node)
+    assert runs is not None, f"{node}: SNAC GPU run not declared in tests/_coverage.py"
+    assert (n_frames, batch) in runs, f"{node}: ({n_frames}, {batch}) is not declared ({runs})"
+
+
 def current_test():
     """'file.py::name[param]' of the running pytest test ('' outside pytest)."""
     node = os.environ.get("PYTEST_CURRENT_TEST", "").rsplit(" ", 1)[0]
