@@ -147,6 +147,12 @@ struct mx_llm {
   int rows_atomic = 1;               // option: residual projections (o-proj, down) at >= 2 rows
                                      // add each K range's partial into h with float atomics
                                      // instead of the split-K seam (mx_rows_v4.inc)
+  int rows_qkv_parts = 1;            // option: decode at >= 2 rows, the qkv GEMM's K ranges
+                                     // store raw partials and the attention launch sums them
+                                     // (scale, RoPE, K / V append): no split-K seam
+  float* qkv_parts = nullptr;        // [qkv_nkc_cap][max_batch][qkv rows]
+  float* qkv_ss = nullptr;           // [qkv_nkc_cap][max_batch]
+  static constexpr int qkv_nkc_cap = 12;
   int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
@@ -286,6 +292,8 @@ extern "C" int mx_llm_create(int device, const mx_llm_config* cfg, mx_llm** out)
       }
   }
   A(x->rows_ws, std::max<size_t>(x->rows_ws_floats, 1));
+  A(x->qkv_parts, (size_t)mx_llm::qkv_nkc_cap * c.max_batch * qkv_rows);
+  A(x->qkv_ss, (size_t)mx_llm::qkv_nkc_cap * c.max_batch);
   A(x->rows_tickets, x->rows_tickets_n);
   A(x->row_slot, c.max_batch);
   A(x->row_pos, c.max_batch);
@@ -619,6 +627,7 @@ struct RowSet {
   int cpw;      // attention chunks per wave (att_cpw_auto)
   int nw;       // attention waves per block
   int nsplit;   // attention splits of the launch (grid x)
+  bool decode;  // decode rows (one position each, own KV slots), not a prefill's prompt rows
 };
 
 static void attach_ws(mx_llm* x, GemvArgs& g) {
@@ -683,11 +692,23 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     g.rope_cos = x->rope_cos; g.rope_sin = x->rope_sin; g.row_slot = rs.slot; g.row_pos = rs.pos;
     g.kcache = kc; g.vcache = vc; g.heads = c.heads; g.kv_heads = c.kv_heads;
     g.max_pos = c.max_pos; g.Q = x->q; g.force_legacy = x->legacy_gemv; g.wpb = x->gemv_wpb;
+    // decode at >= 2 rows: the K ranges' raw partials go to the attention launch (no seam)
+    const bool parts = rs.decode && rs.R >= 2 && x->rows_qkv_parts && !x->legacy_gemv &&
+                       v4::rows_qkv_nkc_v4(g) <= mx_llm::qkv_nkc_cap;
+    if (parts) {
+      g.qkv_parts = x->qkv_parts;
+      g.qkv_ss = x->qkv_ss;
+    }
     PROF_BEGIN(PK_QKV);
     e = launch_gemv(g, EPI_QKV, true, st);
     PROF_END();
     if (e != hipSuccess) break;
     AttnArgs at{};
+    if (parts) {
+      at.qkv_parts = x->qkv_parts; at.qkv_ss = x->qkv_ss; at.qkv_nkc = v4::rows_qkv_nkc_v4(g);
+      at.qkv_n = qkv_rows; at.hidden = H; at.eps = c.eps;
+      at.rope_cos = x->rope_cos; at.rope_sin = x->rope_sin;
+    }
     at.Q = x->q; at.kcache = kc; at.vcache = vc; at.row_slot = rs.slot; at.row_pos = rs.pos;
     at.heads = c.heads; at.kv_heads = c.kv_heads; at.max_pos = c.max_pos;
     at.scale = 1.0f / sqrtf(128.0f);
@@ -825,7 +846,7 @@ static hipError_t enqueue_decode(mx_llm* x, int n_rows, int max_len, int cpw, bo
     const int nw = att_nw_of(x, n_rows, max_len);
     const int S = 32 * nw * cpw;
     RowSet rs{x->h_dec, x->row_slot, x->row_pos, n_rows, max_len, cpw, nw,
-              (max_len + S - 1) / S};
+              (max_len + S - 1) / S, true};
     e = enqueue_layers(x, rs, st, prof);
   }
   PROF_BEGIN(PK_HEAD);
@@ -870,7 +891,7 @@ extern "C" int mx_llm_prefill(mx_llm* x, int slot, int row, const int32_t* ids, 
   MX_TRY(x, launch_embed_rows(x->pre_ids, n, slot, x->embed, c.hidden, c.vocab, x->seen,
                               x->h_pre, st));
   RowSet rs{x->h_pre, x->pre_slot, x->pre_pos, n, n, att_cpw_auto(x, n, n),
-            att_nw_of(x, n, n), 0};
+            att_nw_of(x, n, n), 0, false};
   rs.nsplit = (n + 32 * rs.nw * rs.cpw - 1) / (32 * rs.nw * rs.cpw);
   MX_TRY(x, enqueue_layers(x, rs, st, nullptr));
   MX_TRY(x, hipMemsetAsync(x->best + row, 0, 8, st));
@@ -1346,6 +1367,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
       MX_TRY(x, hipMemset(x->eng_trace, 0, (size_t)1024 * x->c.layers * 12 * 8));
     }
     if (!value) x->eng_trace = nullptr;  // (the buffer stays allocated until destroy)
+  } else if (k == "rows_qkv_parts") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_qkv_parts must be 0 or 1");
+    x->rows_qkv_parts = value;
   } else if (k == "rows_atomic") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_atomic must be 0 or 1");
     x->rows_atomic = value;

@@ -43,6 +43,9 @@ struct GemvArgs {
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
   int rows_atomic;         // generation 4, residual projections split over K: every K range
                            // adds its partial tile into Y with float atomics (no seam)
+  float* qkv_parts;        // generation 4 EPI_QKV, decode: null, or [nkc][R][N] -- every K range
+  float* qkv_ss;           // stores its raw partial (and [nkc][R] partial sums of squares);
+                           // the attention launch sums them, scales, RoPEs and appends K / V
   unsigned long long* trace;  // generation 4 diagnostic: [block][8] phase stamps (null = off)
   int trace_cap;           // blocks the trace buffer holds (stamps of later blocks are dropped)
   int head_b1;             // R = 1 lm_head on the persistent kernel (head_b1.hip; 0 = gemv_kernel)
@@ -86,6 +89,14 @@ struct AttnArgs {
   float* out;              // [R][heads*128]
   int debug;               // timing experiments only (0 in the product path)
   int no_merge;            // 1: every split stores its partial, the consumer merges (R = 1)
+  // multi-row decode with the qkv GEMM's K-range partials (GemvArgs::qkv_parts): q / k / v of
+  // the new position = RoPE(rsqrt(mean x^2 + eps) x sum of the partials), K / V appended here
+  const float* qkv_parts;  // [nkc][R][qkv_n] raw partial sums, packed wqkv row order (null: off)
+  const float* qkv_ss;     // [nkc][R] partial sums of squares of the qkv input
+  int qkv_nkc, qkv_n, hidden;
+  float eps;
+  const float* rope_cos;   // [max_pos][64]
+  const float* rope_sin;
 };
 
 struct CommitArgs {
@@ -114,6 +125,8 @@ hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_
 void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, size_t* tickets);
 // the multi-row o-projection can merge the attention splits itself (attn no_merge)
 bool rows_merge_ok_v4(const GemvArgs& o);
+// K ranges the qkv launch (EPI_QKV, NORM) of these arguments splits into
+int rows_qkv_nkc_v4(const GemvArgs& a);
 }  // namespace v4
 struct SampleArgs {
   const float* logits;     // [R][V] penalised logits (kept by the lm_head epilogue)

@@ -26,6 +26,12 @@ void gemm_rows_workspace_v4(int N, int K, int R, int epi, size_t* ws_floats, siz
 
 bool rows_merge_ok_v4(const GemvArgs& o) { return rows_merge_ok(o); }
 
+int rows_qkv_nkc_v4(const GemvArgs& a) {
+  int mt, nt;
+  rows_tiles(EPI_QKV, a.R, &mt, &nt, a.rows_nt_max);
+  return a.K % 128 ? 1 : rows_nkc(a.N, a.K, a.R, mt, nt, rows_target_of<EPI_QKV>(a));
+}
+
 // R >= 2 rows.  Returns hipErrorNotSupported for shapes the kernel does not cover.
 hipError_t launch_gemm_rows_v4(const GemvArgs& a, int epi, bool norm, hipStream_t st) {
   if (a.R < 1) return hipErrorNotSupported;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6: qkv K-range partials summed by the attention launch (rows_qkv_parts): multi-row
+# parity first, then the A/B, then the whole GPU suite
+set -o pipefail
+O=gpurun_out/r06_d; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -v --timeout 170 --timeout-method thread tests/test_gpu_llm.py -k "batched or straddl" > $O/rows_tests.log 2>&1 || exit 1
+for spec in "8:" "32:" "8:--fp8"; do
+  rows=${spec%%:*}; f=${spec#*:}; tag=r${rows}${f:+f8}
+  timeout -k 10 200 python -u scripts/ab_decode.py --rows $rows $f --pos 600 --rounds 3 --reps 50 --variants seam,qkvseam,base > $O/ab_${tag}.log 2>&1 || exit 2
+done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 3

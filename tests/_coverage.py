@@ -56,7 +56,7 @@ GPU_RUNS = {
     "test_gpu_llm.py::test_batched_decode_orpheus_width_6_rows":
         [_r(ORPHEUS, _rows(6, 6), 6)],
     "test_gpu_llm.py::test_batched_decode_orpheus_width_6_rows_split_k_seam":
-        [_r(ORPHEUS, _rows(6, 6), 6, rows_atomic=0)],
+        [_r(ORPHEUS, _rows(6, 6), 6, rows_atomic=0, rows_qkv_parts=0)],
     "test_gpu_llm.py::test_batched_decode_orpheus_width_32_rows":
         [_r(ORPHEUS, _rows(32, 4), 5)],
     "test_gpu_llm.py::test_batched_decode_orpheus_width_64_rows":
@@ -83,7 +83,7 @@ GPU_RUNS = {
     "test_gpu_fp8.py::test_fp8_batched_orpheus_width_8_rows":
         [_r(ORPHEUS, [5 + 4 * i for i in range(8)], 6, f8=True)],
     "test_gpu_fp8.py::test_fp8_batched_orpheus_width_8_rows_split_k_seam":
-        [_r(ORPHEUS, [5 + 4 * i for i in range(8)], 6, f8=True, rows_atomic=0)],
+        [_r(ORPHEUS, [5 + 4 * i for i in range(8)], 6, f8=True, rows_atomic=0, rows_qkv_parts=0)],
     "test_gpu_fp8.py::test_fp8_lm_head_grid_stride_orpheus_width":
         [_r(ORPHEUS, [40], 12, f8=True, head_b1=0)],
     "test_gpu_fp8.py::test_fp8_batched_orpheus_width_8_rows_split_attention_merged_in_oproj":

@@ -110,13 +110,13 @@ def test_fp8_batched_orpheus_width_8_rows():
 
 
 def test_fp8_batched_orpheus_width_8_rows_split_k_seam():
-    """Option rows_atomic = 0 with e4m3 weights: the residual projections' K ranges merged by
-    the split-K seam (row scales applied by the last arriver) instead of float atomics."""
+    """Options rows_atomic = 0 and rows_qkv_parts = 0 with e4m3 weights: the qkv and residual
+    projections' K ranges merged by the split-K seam (row scales applied by the last arriver)."""
     cfg = C.OrpheusConfig(layers=2)
     qw = quantize_fp8(synthetic_llm_weights(cfg, seed=55), cfg)
     rng = np.random.default_rng(16)
     prompts = [[int(x) for x in rng.integers(1000, 128000, 5 + 4 * i)] for i in range(8)]
-    assert _check(cfg, qw, prompts, 6, options={"rows_atomic": 0}) >= 0.8 * 8 * 6
+    assert _check(cfg, qw, prompts, 6, options={"rows_atomic": 0, "rows_qkv_parts": 0}) >= 0.8 * 8 * 6
 
 
 def test_fp8_lm_head_grid_stride_orpheus_width():

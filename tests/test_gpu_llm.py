@@ -417,12 +417,13 @@ def test_batched_decode_orpheus_width_6_rows():
 
 
 def test_batched_decode_orpheus_width_6_rows_split_k_seam():
-    """Option rows_atomic = 0: the o-proj and down K ranges merged by the split-K seam
-    (write-through partials, ticket, last-arriver merge) instead of float atomics into h."""
+    """Options rows_atomic = 0 and rows_qkv_parts = 0: the qkv, o-proj and down K ranges merged
+    by the split-K seam (write-through partials, ticket, last-arriver merge) instead of float
+    atomics into h (o-proj, down) and the attention launch summing the qkv partials."""
     cfg = _cfgs("orpheus2")
     w = synthetic_llm_weights(cfg, seed=25)
     assert _compare_rows(cfg, w, _orpheus_prompts(6, 26, 6, 1), 6,
-                         options={"rows_atomic": 0}) >= 0.8 * 6 * 6
+                         options={"rows_atomic": 0, "rows_qkv_parts": 0}) >= 0.8 * 6 * 6
 
 
 def test_batched_decode_orpheus_width_32_rows():
