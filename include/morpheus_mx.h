@@ -110,7 +110,8 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
 /* Tuning knobs (capi.hip mx_llm_set_option; unknown keys and out-of-range values fail with
  * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "rows_frag",
- * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_nt_max", "rows_nt1",
+ * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_target_qkv", "rows_target_o",
+ * "rows_target_gu", "rows_target_down" (the target for one kind of layer launch), "rows_nt_max", "rows_nt1",
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "rows_atomic" (o-proj / down at >= 2 rows: K ranges
  * add into the residual with float atomics, no split-K seam), "rows_qkv_parts" (decode at >= 2
  * rows: the qkv K ranges' raw partials summed, scaled, RoPE'd and appended by the attention

@@ -135,6 +135,8 @@ struct mx_llm {
   int rows_pw = 2;                   // option: generation-4 weight prefetch distance (2 measured best)
   int rows_pw_f8 = 2;                // option: the same for e4m3 weights (1, 2)
   int rows_target = 0;               // option: generation-4 K-range split target (0 = per shape)
+  int rows_target_k[4] = {0, 0, 0, 0};  // options rows_target_{qkv,o,gu,down}: the same for
+                                        // one kind of the layer's launches (0 = rows_target)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
   int rows_nt1 = 11;                 // option: kinds whose 17-32-row launches take 16-row batch
                                      // tiles (bit 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head)
@@ -654,6 +656,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
 // (profiles/r05_rows_nt1.log)
 static void nt_cap(const mx_llm* x, GemvArgs& g, int kind_bit, int R) {
   if ((x->rows_nt1 >> kind_bit) & 1 && R <= 32) g.rows_nt_max = 1;
+  if (kind_bit < 4 && x->rows_target_k[kind_bit] > 0) g.rows_target = x->rows_target_k[kind_bit];
 }
 
 // Optional per-launch timing (eager runs only): prof->ev[k] brackets launch class k.
@@ -1412,6 +1415,11 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_head_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_head_target must be 0..4096");
     x->rows_head_target = value;
+  } else if (k == "rows_target_qkv" || k == "rows_target_o" || k == "rows_target_gu" ||
+             k == "rows_target_down") {
+    if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, k + " must be 0..4096");
+    const int kind = k == "rows_target_qkv" ? 0 : k == "rows_target_o" ? 1 : k == "rows_target_gu" ? 2 : 3;
+    x->rows_target_k[kind] = value;
   } else if (k == "rows_target") {
     if (value < 0 || value > 4096) MX_FAIL(x, MX_ERR_ARG, "rows_target must be 0..4096");
     x->rows_target = value;

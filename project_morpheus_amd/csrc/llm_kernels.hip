@@ -561,36 +561,30 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
   // chunks are dealt round-robin over the waves (wave w: chunks w, w + NW, ...), so a split
   // longer than the context still keeps every wave busy with ~equal work
   const int base0 = split * S + wid * 32;
-  if (base0 < L) load_kv(base0, 0);
+  // (qkv_parts: the wave whose first chunk holds the new position loads it only after it has
+  // appended that position, below)
+  const bool late0 = a.qkv_parts != nullptr && base0 == ((L - 1) & ~31);
+  if (base0 < L && !late0) load_kv(base0, 0);
 
   // Multi-row decode after the seam-free qkv GEMM (AttnArgs::qkv_parts): q, k and v of the new
   // position L - 1 are the sums of the qkv launch's K-range partials (range order), scaled by
   // the RMSNorm factor of the summed partial sums of squares, RoPE'd (q, k) -- the epilogue the
   // qkv GEMM's last arriving range ran before (rows_epilogue EPI_QKV).  Every split block
-  // stages its q; the block whose split holds L - 1 also appends the bf16 K / V to the cache.
-  // Its waves' first K / V loads were issued above, before that append: the chunk holding
-  // L - 1 takes the staged k / v in registers instead (patched in chunk() below).
+  // stages its q in LDS.  In the block whose split holds L - 1, the wave that will load the
+  // chunk holding it computes that position's k / v and appends them to the cache itself, so
+  // its own later loads of those addresses are ordered after the stores (one wave: program
+  // order); if that chunk is its first one, its early load above was skipped (late0).
   const bool parts = a.qkv_parts != nullptr;
   __shared__ __attribute__((aligned(16))) float qs[GRP][128];
-  __shared__ __attribute__((aligned(16))) uint16_t kvn[2][128];  // new position: k, v (bf16)
   if (parts) {
     const int N = a.qkv_n, NQ = a.heads * 128, KVD = a.kv_heads * 128, R = gridDim.z;
     const int pos = L - 1;
     float ss = 0.f;
     for (int kc = 0; kc < a.qkv_nkc; ++kc) ss += a.qkv_ss[(size_t)kc * R + r];
     const float scl = 1.0f / sqrtf(ss / (float)a.hidden + a.eps);
-    const bool owner = split == pos / S;
-    uint16_t* kcw = const_cast<uint16_t*>(a.kcache) + head * a.max_pos * 128;
-    uint16_t* vcw = const_cast<uint16_t*>(a.vcache) + head * a.max_pos * 128;
-    for (int i = tid; i < GRP * 64 + 128; i += NT) {
-      // pair i: q head h dims (p, p + 64) | k dims (p, p + 64) | v dims (2p, 2p + 1); the
-      // packed wqkv rows of q / k are pair-interleaved (2p -> dim p, 2p + 1 -> dim p + 64)
-      const int kind = i < GRP * 64 ? 0 : i < GRP * 64 + 64 ? 1 : 2;
-      const int p = kind == 0 ? (i & 63) : (i - GRP * 64 - 64 * (kind - 1));
-      const int h = kind == 0 ? (i >> 6) : 0;
-      const int idx = kind == 0 ? (kvh * GRP + h) * 128 + 2 * p
-                                : (kind == 1 ? NQ : NQ + KVD) + kvh * 128 + 2 * p;
-      float x1 = 0.f, x2 = 0.f;
+    auto pair = [&](int idx, float& x1, float& x2) {
+      x1 = 0.f;
+      x2 = 0.f;
       for (int kc = 0; kc < a.qkv_nkc; ++kc) {
         const float2 v = *reinterpret_cast<const float2*>(a.qkv_parts + ((size_t)kc * R + r) * N + idx);
         x1 += v.x;
@@ -598,30 +592,29 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
       }
       x1 *= scl;
       x2 *= scl;
-      if (kind == 2) {
-        const uint16_t b1 = f32_to_bf16(x1), b2 = f32_to_bf16(x2);
-        kvn[1][2 * p] = b1;
-        kvn[1][2 * p + 1] = b2;
-        if (owner) {
-          vcw[kv_v_off(pos, 2 * p)] = b1;
-          vcw[kv_v_off(pos, 2 * p + 1)] = b2;
-        }
-      } else {
-        const float cs = a.rope_cos[(size_t)pos * 64 + p], sn = a.rope_sin[(size_t)pos * 64 + p];
-        const float o1 = x1 * cs - x2 * sn, o2 = x2 * cs + x1 * sn;
-        if (kind == 0) {
-          qs[h][p] = o1;
-          qs[h][p + 64] = o2;
-        } else {
-          const uint16_t b1 = f32_to_bf16(o1), b2 = f32_to_bf16(o2);
-          kvn[0][p] = b1;
-          kvn[0][p + 64] = b2;
-          if (owner) {
-            kcw[kv_k_off(pos, p)] = b1;
-            kcw[kv_k_off(pos, p + 64)] = b2;
-          }
-        }
-      }
+    };
+    // q: pair (h, p) -> dims p, p + 64 (the packed wqkv rows are pair-interleaved)
+    for (int i = tid; i < GRP * 64; i += NT) {
+      const int h = i >> 6, p = i & 63;
+      float x1, x2;
+      pair((kvh * GRP + h) * 128 + 2 * p, x1, x2);
+      const float cs = a.rope_cos[(size_t)pos * 64 + p], sn = a.rope_sin[(size_t)pos * 64 + p];
+      qs[h][p] = x1 * cs - x2 * sn;
+      qs[h][p + 64] = x2 * cs + x1 * sn;
+    }
+    if (split == pos / S && wid == ((((pos & ~31) - split * S) >> 5) % NW)) {
+      const int p = lane;  // k dims (p, p + 64); v dims (2p, 2p + 1)
+      float k1, k2, v1, v2;
+      pair(NQ + kvh * 128 + 2 * p, k1, k2);
+      pair(NQ + KVD + kvh * 128 + 2 * p, v1, v2);
+      const float cs = a.rope_cos[(size_t)pos * 64 + p], sn = a.rope_sin[(size_t)pos * 64 + p];
+      uint16_t* kcw = const_cast<uint16_t*>(a.kcache) + head * a.max_pos * 128;
+      uint16_t* vcw = const_cast<uint16_t*>(a.vcache) + head * a.max_pos * 128;
+      kcw[kv_k_off(pos, p)] = f32_to_bf16(k1 * cs - k2 * sn);
+      kcw[kv_k_off(pos, p + 64)] = f32_to_bf16(k2 * cs + k1 * sn);
+      vcw[kv_v_off(pos, 2 * p)] = f32_to_bf16(v1);
+      vcw[kv_v_off(pos, 2 * p + 1)] = f32_to_bf16(v2);
+      if (late0) load_kv(base0, 0);
     }
     __syncthreads();
   }
@@ -662,33 +655,6 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
     const int base = base0 + ch * 32 * NW;
     if (base >= L) return false;
     if (ch + 1 < CPW && base + 32 * NW < L) load_kv(base + 32 * NW, cb ^ 1);
-    if (parts && base == ((L - 1) & ~31)) {
-      // the chunk holding the new position (wave-uniform): its k / v come from the staged
-      // values (kv_k_off / kv_v_off: K row rr of tile T, V element qn & 7 of group qn >> 3)
-      const int qn = (L - 1) & 31;
-      const int T = (qn >> 2) & 1, rr = 4 * (qn >> 3) + (qn & 3);
-      if (c == rr) {
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          const uint4 kn = *reinterpret_cast<const uint4*>(&kvn[0][32 * st + 8 * g]);
-          if (T == 0) kf[cb][0][st] = kn;
-          else kf[cb][1][st] = kn;
-        }
-      }
-      if (g == (qn >> 3)) {
-        const int wi = (qn & 7) >> 1;
-        const uint32_t sh = (qn & 1) * 16, keep = ~(0xffffu << sh);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const uint32_t val = (uint32_t)kvn[1][16 * t + c] << sh;
-          uint4& vv = vf[cb][t];
-          if (wi == 0) vv.x = (vv.x & keep) | val;
-          else if (wi == 1) vv.y = (vv.y & keep) | val;
-          else if (wi == 2) vv.z = (vv.z & keep) | val;
-          else vv.w = (vv.w & keep) | val;
-        }
-      }
-    }
     __builtin_amdgcn_sched_barrier(0);
     // scores
     f32x4 sc[2];

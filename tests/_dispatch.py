@@ -130,6 +130,14 @@ def _rows_key(MT, NT, epi, norm, sub, f8, o, nsm=0):
     return f"v4::gemm_rows_kernel<{MT}, {NT}, {epi}, {_b(norm)}, {sub}, {_b(f8)}, {pw}, {nsm}>"
 
 
+def target_opts(o, kind):
+    """capi.hip nt_cap: options rows_target_{qkv,o,gu,down} override rows_target per kind."""
+    names = ("rows_target_qkv", "rows_target_o", "rows_target_gu", "rows_target_down")
+    if kind is not None and kind < 4 and o.get(names[kind], 0) > 0:
+        return dict(o, rows_target=o[names[kind]])
+    return o
+
+
 def nt_max_of(o, kind, R):
     """capi.hip nt_cap: option rows_nt1 puts this kind's 17-32-row launches on 16-row tiles
     (kind: 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head; None: not a layer launch)."""
@@ -141,6 +149,7 @@ def nt_max_of(o, kind, R):
 def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0, kind=None):
     """launch_gemm_rows_v4 -> the instantiation (None where it returns NotSupported)."""
     mt, nt = rows_tiles(R, nt_max_of(o, kind, R))
+    o = target_opts(o, kind)
     if epi == EPI_ARGMAX and norm and o["rows_head_mt"] == 2 and nt in (1, 2):
         mt = 2
     if K % 128:
@@ -157,6 +166,7 @@ def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0, kind=None):
 
 def rows_merge_ok(d, R, nsplit, o):
     mt, nt = rows_tiles(R, nt_max_of(o, 1, R))
+    o = target_opts(o, 1)
     K = d.heads * 128
     if R < 2 or nt != 1 or K % 128 or nsplit < 1 or nsplit > 4:
         return False
