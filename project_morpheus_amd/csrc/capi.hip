@@ -138,8 +138,10 @@ struct mx_llm {
   int rows_target_k[4] = {0, 0, 0, 0};  // options rows_target_{qkv,o,gu,down}: the same for
                                         // one kind of the layer's launches (0 = rows_target)
   int rows_nt_max = 0;               // option: generation-4 batch-tile cap in 16-row units (0 = 4)
-  int rows_nt1 = 11;                 // option: kinds whose 17-32-row launches take 16-row batch
-                                     // tiles (bit 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head)
+  int rows_nt1 = 2;                  // option: kinds whose 17-32-row launches take 16-row batch
+                                     // tiles (bit 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head;
+                                     // round 5: 11; with the seam-free qkv / down of round 6 the
+                                     // o-proj alone is best: profiles/r06_rows_nt1.log)
   int rows_head_target = 0;          // option: lm_head K-range target (0 = default)
   int rows_head_mt = 1;              // option: multi-row lm_head weight rows per wave / 16
                                      // (1 since round 5: with one argmax atomic per block the

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "att_nw_batch": 8,
             "gemv_wpb": 4, "rpw_o": 0, "rpw_gu": 0, "rpw_down": 0, "rows_lds_pad": 0,
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
-            "rows_head_mt": 1, "rows_head_target": 0, "rows_nt_max": 0, "rows_nt1": 11, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0, "rows_atomic": 1, "rows_qkv_parts": 1,
+            "rows_head_mt": 1, "rows_head_target": 0, "rows_nt_max": 0, "rows_nt1": 2, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0, "rows_atomic": 1, "rows_qkv_parts": 1,
             "rows_target_qkv": 0, "rows_target_o": 0, "rows_target_gu": 0, "rows_target_down": 0}
 VARIANTS = {
     "base": {},
@@ -41,6 +41,9 @@ VARIANTS = {
     "hmt1": {"rows_head_mt": 1},
     "hmt2": {"rows_head_mt": 2},
     "nt1_none": {"rows_nt1": 0},
+    "nt1_q": {"rows_nt1": 1},
+    "nt1_d": {"rows_nt1": 8},
+    "nt1_qd": {"rows_nt1": 9},
     "nt1_o": {"rows_nt1": 2},
     "nt1_oq": {"rows_nt1": 3},
     "nt1_od": {"rows_nt1": 10},

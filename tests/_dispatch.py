@@ -45,7 +45,7 @@ FP8_SMALL = Dims(1024, 8, 2, 2048, 1000)
 # library option defaults (capi.hip struct mx_llm)
 DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
-                rows_nt_max=0, rows_nt1=11, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
+                rows_nt_max=0, rows_nt1=2, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
                 rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7, rows_atomic=1,
                 rows_qkv_parts=1)
 # (rows_atomic and rows_qkv_parts select the residual projections' split-K epilogue at run time inside the same
