@@ -26,6 +26,8 @@ VARIANTS = {
     "cpw2": {"att_cpw": 2},
     "cpw2_rpw_o2": {"att_cpw": 2, "rpw_o": 2},
     "rpw_gu4": {"rpw_gu": 4},
+    "rpw_gu2": {"rpw_gu": 2},
+    "wpb8_down2": {"gemv_wpb": 8, "rpw_down": 2},
     "rpw_down2": {"rpw_down": 2},
     "wpb8": {"gemv_wpb": 8},
     "gu4_down2": {"rpw_gu": 4, "rpw_down": 2},
