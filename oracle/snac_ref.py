@@ -109,12 +109,12 @@ def _mix64(z: np.ndarray) -> np.ndarray:
     return z ^ (z >> np.uint64(31))
 
 
-def device_noise(seed: int, n: int) -> np.ndarray:
+def device_noise(seed: int, j) -> np.ndarray:
     """Restatement of the GPU's NoiseBlock noise for a window seeded ``seed`` (csrc/
-    snac_kernels.hip gauss_kernel): element j = Box-Muller of mix64(seed ^ mix64(j)), float32.
+    snac_kernels.hip gauss_at): element key j = Box-Muller of mix64(seed ^ mix64(j)), float32.
     Lets the end-to-end tests compare audio with the noise ON (host libm vs device ulps)."""
     with np.errstate(over="ignore"):
-        j = np.arange(n, dtype=np.uint64)
+        j = np.asarray(j, dtype=np.uint64)
         h = _mix64(np.uint64(seed) ^ _mix64(j))
     u1 = ((h >> np.uint64(40)).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777217.0)
     u2 = ((h >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.float32) * np.float32(1.0 / 16777216.0)
@@ -123,10 +123,11 @@ def device_noise(seed: int, n: int) -> np.ndarray:
 
 
 def window_noise(seed: int, n_frames: int) -> List[torch.Tensor]:
-    """The four NoiseBlock inputs [1,1,T_b] of one window drawn as the device draws them."""
-    z = device_noise(seed, sum(noise_lengths(n_frames)))
-    out, off = [], 0
-    for t in noise_lengths(n_frames):
-        out.append(torch.from_numpy(z[off:off + t].copy()).reshape(1, 1, t))
-        off += t
+    """The four NoiseBlock inputs [1,1,T_b] of one window drawn as the device draws them: the
+    value at (NoiseBlock s, position t) is keyed j = s << 24 | t (gauss_at), so a window decoded
+    with fewer frames shares the full window's noise at every common position."""
+    out = []
+    for s, t in enumerate(noise_lengths(n_frames)):
+        j = (np.uint64(s) << np.uint64(24)) | np.arange(t, dtype=np.uint64)
+        out.append(torch.from_numpy(device_noise(seed, j)).reshape(1, 1, t))
     return out

@@ -47,7 +47,7 @@ import torch
 from . import _lib
 from .config import BATCH_DEPTH, SNAC_MAX_HOLD, SNAC_MIN_BATCH, STOP_IDS
 from .engine import SAMPLES_PER_FRAME, SLICE_HI, SLICE_LO, LlmEngine, SnacDecoder
-from .schedule import WindowScheduler, code_of_id
+from .schedule import WindowScheduler, code_of_id, frames_for_slice
 
 _MASK48 = 0xFFFFFFFFFFFF
 
@@ -419,8 +419,10 @@ class BatchSynthesizer:
         def launch_windows(due: List):
             """due: [(req, window index, codes)] -> one SNAC call per frame-count group."""
             groups: Dict[int, List] = {}
-            for item in due:
-                groups.setdefault(len(item[2]) // 7, []).append(item)
+            for item in due:  # grouped by the frames the kept slice depends on (7 -> 5)
+                n = len(item[2]) // 7
+                groups.setdefault(frames_for_slice(n, min(SLICE_HI, SAMPLES_PER_FRAME * n)),
+                                  []).append(item)
             for nf, items in groups.items():
                 for s in range(0, len(items), self.ring.max_batch):
                     chunk = items[s:s + self.ring.max_batch]

@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 from .config import ENGINE_OPTIONS, STOP_IDS, OrpheusConfig, rope_tables
-from .schedule import WindowScheduler, code_of_id
+from .schedule import WindowScheduler, code_of_id, frames_for_slice
 
 SAMPLES_PER_FRAME = 2048
 SLICE_LO, SLICE_HI = 2048, 4096
@@ -343,9 +343,9 @@ class Synthesizer:
             i = self._windows % self.ring.n
             if len(pending) >= self.ring.n:
                 yield from drain(block=True, upto=1)
-            nf = len(win) // 7
+            lo, hi = SLICE_LO, min(SLICE_HI, SAMPLES_PER_FRAME * (len(win) // 7))
+            nf = frames_for_slice(len(win) // 7, hi)  # the frames the kept slice depends on
             self.ring.codes[i][: 7 * nf] = win[: 7 * nf]
-            lo, hi = SLICE_LO, min(SLICE_HI, SAMPLES_PER_FRAME * nf)
             self.snac.decode_ptr(self.ring.codes_dev[i], nf, 1, 0,
                                  (nseed * 1000003 + widx[0]) & 0xFFFFFFFFFFFF,
                                  self.ring.pcm_dev[i], 0, lo, max(lo, hi), self.snac_stream)

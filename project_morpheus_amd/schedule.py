@@ -12,6 +12,7 @@ tests/golden/speechpipe_golden.json, generated from the reference module):
   Codes <= 0 are not accepted (``token > 0``, :215) and so shift the 7-phase.
 * ``window_valid``     = the range check of ``convert_to_audio`` (:108-111): codes in
   [0, 4096] (4096 passes the check although the codebook has 4096 rows).
+* ``frames_for_slice`` = how many of a window's frames the kept PCM slice depends on.
 """
 from __future__ import annotations
 
@@ -55,6 +56,23 @@ def window_valid(win: List[int]) -> bool:
         if v < 0 or v > 4096:
             return False
     return True
+
+
+# SNAC's receptive field reaches fewer than RIGHT_CONTEXT_FRAMES frames (3 x 2,048 samples)
+# past the end of an output span: in the 24 kHz decoder the input depthwise conv (k7 over 4
+# latent steps per frame), the four polyphase ConvTransposes and their dilated (1, 3, 9) k7
+# residual units add up to less than that.  Measured on the oracle (tests/test_oracle_snac.py):
+# perturbing frames 5 and 6 of a 7-frame window leaves samples [2048, 4096) bit-identical, and
+# decoding frames 0-4 alone (NoiseBlock noise keyed by position, so shared) gives them within
+# 5e-6 (fp32 summation order of the shorter convolutions).
+SAMPLES_PER_FRAME = 2048
+RIGHT_CONTEXT_FRAMES = 3
+
+
+def frames_for_slice(n_frames: int, hi: int) -> int:
+    """Frames of an ``n_frames`` window that samples [.., hi) depend on: the 49-code window
+    speechpipe keeps [2048, 4096) of is decoded as its first 5 frames (2/7 less SNAC work)."""
+    return min(n_frames, -(-hi // SAMPLES_PER_FRAME) + RIGHT_CONTEXT_FRAMES)
 
 
 def deinterleave(win: List[int]):

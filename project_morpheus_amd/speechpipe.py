@@ -22,7 +22,7 @@ from typing import AsyncIterator, List, Optional
 
 import numpy as np
 
-from .schedule import WindowScheduler, parse_token_text, window_valid
+from .schedule import WindowScheduler, frames_for_slice, parse_token_text, window_valid
 
 snac_device = "cuda"
 CUSTOM_TOKEN_PREFIX = "<custom_token_"
@@ -62,6 +62,8 @@ def convert_to_audio(multiframe: List[int], count: int) -> Optional[bytes]:
         raise IndexError("index out of range in self (SNAC codebook has 4096 entries)")
     import torch
     m = _get_model()
+    # only the frames the kept samples [2048, 4096) depend on (schedule.frames_for_slice)
+    win = win[: 7 * frames_for_slice(nf, min(4096, 2048 * nf))]
     codes = torch.tensor(win, dtype=torch.int32, device=f"cuda:{m.device}").reshape(1, -1)
     _seed[0] += 1
     pcm, _ = m.decode(codes, seed=_seed[0])

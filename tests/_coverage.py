@@ -114,7 +114,8 @@ GPU_RUNS = {
 # them against the serving envelope and the bench trace)
 SNAC_RUNS = {
     **{f"test_gpu_snac.py::test_snac_window_parity[{n}-{b}]": [(n, b)]
-       for n, b in ((1, 1), (4, 1), (7, 1), (7, 3), (2, 2), (1, 5), (4, 9), (7, 12))},
+       for n, b in ((1, 1), (4, 1), (7, 1), (7, 3), (2, 2), (1, 5), (4, 9), (7, 12), (5, 1),
+                    (5, 12))},
     "test_gpu_snac.py::test_snac_batched_32_windows_matches_oracle": [(7, 32)],
 }
 

@@ -80,9 +80,10 @@ def window_keys(n_frames, B):
 
 
 # The window shapes the serving path decodes (schedule.WindowScheduler: the first window is 7
-# codes = 1 frame, then 28 or 49 codes = 4 or 7 frames, the end-of-stream flush 4 or 7), in
-# batches of 1 (engine.Synthesizer) up to the SNAC decoder's max_batch (bench.py: 32).
-SERVING_FRAMES = (1, 4, 7)
+# codes = 1 frame, then 28 or 49 codes = 4 or 7 frames, the end-of-stream flush 4 or 7; a
+# 7-frame window is decoded as its first 5 frames, schedule.frames_for_slice), in batches of 1
+# (engine.Synthesizer) up to the SNAC decoder's max_batch (bench.py: 32).
+SERVING_FRAMES = (1, 4, 5)
 
 
 def envelope(max_batch=32, frames=SERVING_FRAMES):

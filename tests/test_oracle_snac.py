@@ -63,3 +63,39 @@ def test_synthetic_shapes_cover_decoder():
     assert set(w) == set(snac_shapes())
     n = sum(v.numel() for k, v in w.items())
     assert 12.5e6 < n < 14.5e6   # ~13 M decoder + quantizer params
+
+
+def _decode_window(w, codes, n, noise):
+    c0 = [codes[7 * f] for f in range(n)]
+    c1 = [codes[7 * f + j] for f in range(n) for j in (1, 4)]
+    c2 = [codes[7 * f + j] for f in range(n) for j in (2, 3, 5, 6)]
+    return snac_ref.decode(w, c0, c1, c2, noise=noise).reshape(-1)
+
+
+def test_kept_slice_depends_on_the_first_five_frames_only():
+    """schedule.frames_for_slice: the samples speechpipe keeps of a 49-code window, [2048, 4096)
+    (speechpipe.py:122), do not depend on frames 5 and 6 (bit-identical when they change), so the
+    serving path decodes the window's first 5 frames; with the NoiseBlock noise keyed by
+    position (window_noise, the device's gauss_at) that decode gives the kept samples within
+    fp32 summation order of the full one.  Frame 4 does reach them (the bound is tight)."""
+    import numpy as np
+
+    from project_morpheus_amd.schedule import frames_for_slice
+    w = synthetic_snac_weights(seed=3)
+    rng = np.random.default_rng(0)
+    codes = [int(v) for v in rng.integers(0, 4096, 49)]
+    full = _decode_window(w, codes, 7, snac_ref.window_noise(11, 7))[2048:4096]
+    late = list(codes)
+    for k in range(35, 49):
+        late[k] = int(rng.integers(0, 4096))
+    assert torch.equal(_decode_window(w, late, 7, snac_ref.window_noise(11, 7))[2048:4096], full)
+    early = list(codes)
+    for k in range(28, 35):
+        early[k] = int(rng.integers(0, 4096))
+    assert float((_decode_window(w, early, 7, snac_ref.window_noise(11, 7))[2048:4096] - full)
+                 .abs().max()) > 1e-3
+    n = frames_for_slice(7, 4096)
+    assert n == 5 and frames_for_slice(4, 4096) == 4 and frames_for_slice(1, 2048) == 1
+    short = _decode_window(w, codes[: 7 * n], n, snac_ref.window_noise(11, n))[2048:4096]
+    d = (short - full).abs()
+    assert float(d.max()) < 2e-5 and float(d.pow(2).mean().sqrt()) < 5e-6
