@@ -43,6 +43,8 @@ struct GemvArgs {
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
   int rows_atomic;         // generation 4, residual projections split over K: every K range
                            // adds its partial tile into Y with float atomics (no seam)
+  int rows_order;          // generation 4 block order: 0 K range, weight tile, batch tile;
+                           // 1 K range, batch tile, weight tile
   float* qkv_parts;        // generation 4 EPI_QKV, decode: null, or [nkc][R][N] -- every K range
   float* qkv_ss;           // stores its raw partial (and [nkc][R] partial sums of squares);
                            // the attention launch sums them, scales, RoPEs and appends K / V

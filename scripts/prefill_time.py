@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--lens", default="16,64,128,256,512")
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value")
     args = ap.parse_args()
     import torch
     from project_morpheus_amd import config as C
@@ -33,6 +34,9 @@ def main():
                     max_prefill=max(lens), wdtype="fp8" if args.fp8 else "bf16")
     del w
     torch.cuda.empty_cache()
+    for kv in args.opt:
+        k, v = kv.split("=")
+        llm.set_option(k, int(v))
     st = torch.cuda.Stream()
     params = 3_300_864_000
     for n in lens:
@@ -46,7 +50,7 @@ def main():
         e1.record(st)
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
-        print(json.dumps({"n": n, "wdtype": "fp8" if args.fp8 else "bf16", "ms": round(ms, 3),
+        print(json.dumps({"n": n, "opts": args.opt, "wdtype": "fp8" if args.fp8 else "bf16", "ms": round(ms, 3),
                           "TFLOP/s": round(2 * params * n / (ms * 1e-3) / 1e12, 1)}), flush=True)
 
 
