@@ -115,8 +115,7 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * "rows_pw", "rows_pw_f8", "rows_lds_pad", "rows_atomic" (o-proj / down at >= 2 rows: K ranges
  * add into the residual with float atomics, no split-K seam), "rows_qkv_parts" (decode at >= 2
  * rows: the qkv K ranges' raw partials summed, scaled, RoPE'd and appended by the attention
- * launch, no split-K seam), "rows_order" (1: the batch tiles of one weight tile dispatched
- * together), "b1_engine" (one-row steps as ONE persistent
+ * launch, no split-K seam), "b1_engine" (one-row steps as ONE persistent
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
  * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline),
  * "engine_timeout" (bound of every engine wait, 100 MHz ticks; 0 = 50 ms), "engine_dbg" (timing

@@ -151,14 +151,12 @@ struct mx_llm {
   int rows_atomic = 1;               // option: residual projections (o-proj, down) at >= 2 rows
                                      // add each K range's partial into h with float atomics
                                      // instead of the split-K seam (mx_rows_v4.inc)
-  int rows_order = 0;                // option: generation-4 block order (1: batch tiles of one
-                                     // weight tile dispatched together)
   int rows_qkv_parts = 1;            // option: decode at >= 2 rows, the qkv GEMM's K ranges
                                      // store raw partials and the attention launch sums them
                                      // (scale, RoPE, K / V append): no split-K seam
   float* qkv_parts = nullptr;        // [qkv_nkc_cap][max_batch][qkv rows]
   float* qkv_ss = nullptr;           // [qkv_nkc_cap][max_batch]
-  static constexpr int qkv_nkc_cap = 12;
+  static constexpr int qkv_nkc_cap = ATT_QKV_NKC_MAX;  // more ranges: the seam qkv
   int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
@@ -645,7 +643,6 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_head_target = x->rows_head_target;
   g.rows_head_mt = x->rows_head_mt;
   g.rows_atomic = x->rows_atomic;
-  g.rows_order = x->rows_order;
   g.head_b1 = x->head_b1;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -1375,9 +1372,6 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
       MX_TRY(x, hipMemset(x->eng_trace, 0, (size_t)1024 * x->c.layers * 12 * 8));
     }
     if (!value) x->eng_trace = nullptr;  // (the buffer stays allocated until destroy)
-  } else if (k == "rows_order") {
-    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_order must be 0 or 1");
-    x->rows_order = value;
   } else if (k == "rows_qkv_parts") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_qkv_parts must be 0 or 1");
     x->rows_qkv_parts = value;

@@ -579,16 +579,30 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
   if (parts) {
     const int N = a.qkv_n, NQ = a.heads * 128, KVD = a.kv_heads * 128, R = gridDim.z;
     const int pos = L - 1;
+    // every range's loads issued at once (clamped addresses, fixed trip count), summed in
+    // range order: a runtime loop here was one dependent round trip per range
+    const int nk = a.qkv_nkc;
+    float ssv[ATT_QKV_NKC_MAX];
+#pragma unroll
+    for (int kc = 0; kc < ATT_QKV_NKC_MAX; ++kc) ssv[kc] = a.qkv_ss[(size_t)min(kc, nk - 1) * R + r];
     float ss = 0.f;
-    for (int kc = 0; kc < a.qkv_nkc; ++kc) ss += a.qkv_ss[(size_t)kc * R + r];
+#pragma unroll
+    for (int kc = 0; kc < ATT_QKV_NKC_MAX; ++kc)
+      if (kc < nk) ss += ssv[kc];
     const float scl = 1.0f / sqrtf(ss / (float)a.hidden + a.eps);
     auto pair = [&](int idx, float& x1, float& x2) {
+      float2 v[ATT_QKV_NKC_MAX];
+#pragma unroll
+      for (int kc = 0; kc < ATT_QKV_NKC_MAX; ++kc)
+        v[kc] = *reinterpret_cast<const float2*>(a.qkv_parts + ((size_t)min(kc, nk - 1) * R + r) * N + idx);
       x1 = 0.f;
       x2 = 0.f;
-      for (int kc = 0; kc < a.qkv_nkc; ++kc) {
-        const float2 v = *reinterpret_cast<const float2*>(a.qkv_parts + ((size_t)kc * R + r) * N + idx);
-        x1 += v.x;
-        x2 += v.y;
+#pragma unroll
+      for (int kc = 0; kc < ATT_QKV_NKC_MAX; ++kc) {
+        if (kc < nk) {
+          x1 += v[kc].x;
+          x2 += v[kc].y;
+        }
       }
       x1 *= scl;
       x2 *= scl;
@@ -628,9 +642,12 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(AttnArgs a) {
     for (int st = 0; st < 4; ++st) {
       float x[8];
       float4 lo, hi;
-      if (parts) {
-        lo = *reinterpret_cast<const float4*>(&qs[hq][32 * st + 8 * g]);
-        hi = *reinterpret_cast<const float4*>(&qs[hq][32 * st + 8 * g + 4]);
+      if (parts) {  // (LDS-typed pointer: a generic one would make these flat loads)
+        typedef const __attribute__((address_space(3))) f32x4 lds_f4;
+        const f32x4 l4 = *(lds_f4*)(&qs[hq][32 * st + 8 * g]);
+        const f32x4 h4 = *(lds_f4*)(&qs[hq][32 * st + 8 * g + 4]);
+        lo = make_float4(l4[0], l4[1], l4[2], l4[3]);
+        hi = make_float4(h4[0], h4[1], h4[2], h4[3]);
       } else {
         lo = *reinterpret_cast<const float4*>(qb + 32 * st);
         hi = *reinterpret_cast<const float4*>(qb + 32 * st + 4);

@@ -12,6 +12,7 @@ constexpr int ATT_S_MIN = 128;      // smallest split (positions) = 4 waves x 32
 constexpr int ATT_MAX_SPLITS = 256; // splits one launch may merge
 constexpr int ATT_MAXG = 4;         // max q-heads per kv-head
 constexpr int ATT_MERGE_CHUNK = 16; // splits whose partials the merging block prefetches
+constexpr int ATT_QKV_NKC_MAX = 8;  // qkv K ranges the attention sums (AttnArgs::qkv_parts)
 
 struct GemvArgs {
   const void* W;           // [N][K] bf16 (WT_BF16) or e4m3 bytes (WT_FP8), packed row order
@@ -43,8 +44,6 @@ struct GemvArgs {
   int rows_head_mt;        // R >= 2 lm_head: weight rows per wave in 16-row units (1 or 2)
   int rows_atomic;         // generation 4, residual projections split over K: every K range
                            // adds its partial tile into Y with float atomics (no seam)
-  int rows_order;          // generation 4 block order: 0 K range, weight tile, batch tile;
-                           // 1 K range, batch tile, weight tile
   float* qkv_parts;        // generation 4 EPI_QKV, decode: null, or [nkc][R][N] -- every K range
   float* qkv_ss;           // stores its raw partial (and [nkc][R] partial sums of squares);
                            // the attention launch sums them, scales, RoPEs and appends K / V
