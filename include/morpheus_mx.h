@@ -119,7 +119,8 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
  * launch, engine_b1.hip), "engine_slots" (its LDS ring slots), "engine_depth" (ring slots in
  * flight per loader wave, 2 or 3), "engine_loaders" (loader waves, 1 or 2), "engine_trace" (record the engine's phase timeline),
  * "engine_timeout" (bound of every engine wait, 100 MHz ticks; 0 = 50 ms), "engine_dbg" (timing
- * experiments: 1 = no hand-off waits, 2 = no weight stream; outputs invalid).  Drops
+ * experiments: 1 = no hand-off waits, 2 = no weight stream; outputs invalid), "bench_one_layer"
+ * (diagnostic: the GEMV probes below sweep layer 0 only, its weights resident on die).  Drops
  * the captured graphs so the next mx_llm_decode re-captures with the new choice. */
 int mx_llm_set_option(mx_llm* ctx, const char* key, int value);
 /* Diagnostic (option engine_trace on): after a device sync, copy the last engine launch's

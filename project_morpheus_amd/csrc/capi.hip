@@ -157,7 +157,9 @@ struct mx_llm {
   float* qkv_parts = nullptr;        // [qkv_nkc_cap][max_batch][qkv rows]
   float* qkv_ss = nullptr;           // [qkv_nkc_cap][max_batch]
   static constexpr int qkv_nkc_cap = ATT_QKV_NKC_MAX;  // more ranges: the seam qkv
-  int head_b1 = 1;                   // option: one-row lm_head on the persistent kernel
+  int bench_one_layer = 0;           // diagnostic option: the GEMV probes sweep layer 0 only
+                                     // (weights resident in the Infinity Cache: the on-die bound)
+  int head_b1 = 1;                  // option: one-row lm_head on the persistent kernel
                                      // (measured -24 us bf16 / -45 us e4m3 per step, round 4)
   int rpw_o = 0, rpw_gu = 0, rpw_down = 0;  // options: rows per wave (0 = default)
   // persistent one-row engine (engine_b1.hip): option b1_engine runs the layers of a
@@ -1118,6 +1120,12 @@ static GemvArgs bench_args(mx_llm* x, int which, int li, int n_rows, int merge_p
   // the step's batch-tile choice (option rows_nt1) for this kind: 0-3 as listed, 4 is the
   // one-row o-proj (kind bit 1), 5 the lm_head (kind bit 4)
   nt_cap(x, g, which == 5 ? 4 : which == 4 ? 1 : which, n_rows);
+  // the multi-row qkv as the decode step launches it: raw K-range partials, no seam
+  if (which == 0 && n_rows >= 2 && x->rows_qkv_parts && !x->legacy_gemv &&
+      v4::rows_qkv_nkc_v4(g) <= mx_llm::qkv_nkc_cap) {
+    g.qkv_parts = x->qkv_parts;
+    g.qkv_ss = x->qkv_ss;
+  }
   return g;
 }
 
@@ -1146,7 +1154,7 @@ static int bench_gemv_impl(mx_llm* x, int which, int n_rows, int reps, float* us
     MX_TRY(x, hipMemcpy(x->row_slot, slots.data(), n_rows * 4, hipMemcpyHostToDevice));
     MX_TRY(x, hipMemcpy(x->row_pos, pos.data(), n_rows * 4, hipMemcpyHostToDevice));
   }
-  auto args = [&](int li) { return bench_args(x, which, li, n_rows, merge_pos); };
+  auto args = [&](int li) { return bench_args(x, which, x->bench_one_layer ? 0 : li, n_rows, merge_pos); };
   const int epi = which == 0 ? EPI_QKV : which == 2 ? EPI_SILU : which == 5 ? EPI_ARGMAX : EPI_RESID;
   const bool norm = which == 0 || which == 2 || which == 5;
   MX_TRY(x, launch_gemv(args(0), epi, norm, st));
@@ -1357,6 +1365,9 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     x->engine_slots = slots;
     x->engine_depth = depth;
     x->b1_engine = en ? 1 : 0;
+  } else if (k == "bench_one_layer") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "bench_one_layer must be 0 or 1");
+    x->bench_one_layer = value;
   } else if (k == "engine_timeout") {
     // (tests force a give-up with a tiny bound; 0 restores the default)
     if (value < 0) MX_FAIL(x, MX_ERR_ARG, "engine_timeout must be >= 0 (ticks of 100 MHz; 0 = 50 ms)");

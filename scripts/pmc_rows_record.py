@@ -1,9 +1,9 @@
-"""Build profiles/r05_pmc_rows{8,8fp8,32}.json from scripts/gpu_pmc_rows_kinds.sh summaries:
+"""Build profiles/rNN_pmc_rows{8,8fp8,32}.json from scripts/gpu_pmc_rows_kinds.sh summaries:
 per projection kind of the multi-row GEMM (generation 4), HBM read / write bytes per launch
 (FETCH_SIZE x 1024 x 2, gfx950 correction; WRITE_SIZE x 1024) against the weight bytes, and the
 SQ pass (wait / issue / MFMA fractions of wave cycles).
 
-    python scripts/pmc_rows_record.py OUT_DIR"""
+    python scripts/pmc_rows_record.py OUT_DIR [ROUND_PREFIX, default r06]"""
 import json
 import os
 import re
@@ -21,13 +21,14 @@ def kind_of(name):
         return "qkv"
     if epi == 2:
         return "gate_up"
-    if epi == 1:
-        return "o_proj" if sub == 3 else "down"
+    if epi == 1:  # K = 3,072 (o-proj) has 24 sub-chunks, K = 8,192 (down) 64
+        return "o_proj" if sub % 3 == 0 else "down"
     return None
 
 
 def main():
     out_dir = sys.argv[1]
+    prefix = sys.argv[2] if len(sys.argv) > 2 else "r06"
     for tag, esz in (("rows8", 2), ("rows8fp8", 1), ("rows32", 2)):
         weights = {"qkv": QKV * H * esz, "o_proj": H * H * esz, "gate_up": 2 * F * H * esz,
                    "down": H * F * esz}
@@ -61,7 +62,7 @@ def main():
                              ("SQ_ACTIVE_INST_ANY", "active_inst_frac")):
                     if c in e:
                         e[f] = round(e[c] / wc, 4)
-        path = os.path.join(out_dir, f"r05_pmc_{tag}.json")
+        path = os.path.join(out_dir, f"{prefix}_pmc_{tag}.json")
         json.dump(rec, open(path, "w"), indent=1)
         print(path, json.dumps({k: {x: v.get(x) for x in ("read_over_weight_bytes", "wait_any_frac",
                                                           "active_inst_frac")}
