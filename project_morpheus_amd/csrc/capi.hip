@@ -127,6 +127,12 @@ struct mx_llm {
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
+  int att_nw6 = 1;                      // option: multi-row attention may take 6-wave blocks
+                                        // (8 rows, L 300-1100: -0.3..-0.7 % per step, bf16 and
+                                        // e4m3; profiles/r06_att_nw6_gemv_balance.log)
+  int gemv_balance = 1;                 // option: one-row qkv / merging o-proj grids balanced
+  int cus = 0;                          //   over the CUs (this many; mx_llm_finalize); bf16 step
+                                        //   -1.0 %, e4m3 -0.3 % (the same log)
   int o_merge = 1;     // option: one-row o-proj merges the attention splits (0 = ticket merge)
   int rows_merge = 1;  // option: the same at 2-16 rows (generation-4 o-proj, rows_merge_ok):
                        // 8 e4m3 rows 1.654 -> 1.637 ms, bf16 8 / 4 / 16 rows unchanged (+-0.1 %)
@@ -549,6 +555,8 @@ extern "C" int mx_llm_finalize(mx_llm* x) {
   if ((!x->c.tied || f8) && !x->lm_loaded) MX_FAIL(x, MX_ERR_STATE, "lm_head not loaded");
   if (f8 && !x->lm_scaled) MX_FAIL(x, MX_ERR_STATE, "lm_head fp8 scales not loaded");
   if (!x->rope_cos) MX_FAIL(x, MX_ERR_STATE, "rope table not set");
+  MX_TRY(x, hipSetDevice(x->device));
+  MX_TRY(x, hipDeviceGetAttribute(&x->cus, hipDeviceAttributeMultiprocessorCount, x->device));
   // fragment-major copies of every matrix the multi-row GEMM streams (2x the weight bytes
   // in HBM, 13.2 GB for Orpheus-3B bf16; the one-row GEMVs keep reading the row-major ones)
   if (!x->lm_f) {
@@ -607,21 +615,41 @@ static void att_b1_shape(const mx_llm* x, int max_len, int* nw, int* cpw) {
   }
 }
 
-static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
-  if (R == 1) {
-    int nw = 4, cpw = 1;
-    att_b1_shape(x, max_len, &nw, &cpw);
-    return cpw;
+// Multi-row steps: (waves per block, chunks per wave) of the attention launch.
+static void att_batch_shape(const mx_llm* x, int R, int max_len, int* nw, int* cpw) {
+  *nw = x->att_nw_batch;
+  if (x->att_cpw_batch > 0) {
+    *cpw = x->att_cpw_batch;
+    return;
   }
-  if (x->att_cpw_batch > 0) return x->att_cpw_batch;
-  const int nw = x->att_nw_batch;
   const int pairs = R * x->c.kv_heads;
   // one split above 64 (row, kv-head) pairs: at 16 rows x 8 kv heads two splits + the ticket
   // merge took 1.966 ms per fp8 step against 1.846 for one split; at 8 rows the 3-split
   // choice and one split are equal (1.752 / 1.763 ms; profiles/r03_attn_rows_split_ab.log)
   const int splits = pairs > 64 ? 1 : std::max(1, 256 / pairs);
   const int chunks = (max_len + 31) / 32;
-  return att_cpw_pick((chunks + splits * nw - 1) / (splits * nw), nw);
+  if (x->att_nw6 && splits > 1) {
+    // option att_nw6: the shortest split (6- or 8-wave blocks) that covers the context in
+    // <= `splits` splits: more blocks, fewer KV bytes per block (at 8 rows, L 600: 4 splits of
+    // 192 positions instead of 3 of 256)
+    static const int shapes[][2] = {{6, 1}, {8, 1}, {6, 2}, {8, 2}, {6, 3}, {8, 3}, {8, 4}, {8, 6}, {8, 8}};
+    for (const auto& sh : shapes) {
+      *nw = sh[0];
+      *cpw = sh[1];
+      if ((chunks + sh[0] * sh[1] - 1) / (sh[0] * sh[1]) <= splits) return;
+    }
+    return;
+  }
+  *cpw = att_cpw_pick((chunks + splits * *nw - 1) / (splits * *nw), *nw);
+}
+
+static int att_cpw_auto(const mx_llm* x, int R, int max_len) {
+  int nw = 4, cpw = 1;
+  if (R == 1)
+    att_b1_shape(x, max_len, &nw, &cpw);
+  else
+    att_batch_shape(x, R, max_len, &nw, &cpw);
+  return cpw;
 }
 
 struct RowSet {
@@ -645,6 +673,7 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
   g.rows_head_target = x->rows_head_target;
   g.rows_head_mt = x->rows_head_mt;
   g.rows_atomic = x->rows_atomic;
+  g.gemv_cus = x->gemv_balance ? x->cus : 0;
   g.head_b1 = x->head_b1;
   g.ws = x->rows_ws;
   g.ws_floats = x->rows_ws_floats;
@@ -808,9 +837,11 @@ static int decode_max_len(const mx_llm* x, int n_rows) {
 }
 
 static int att_nw_of(const mx_llm* x, int R, int max_len) {
-  if (R != 1) return x->att_nw_batch;
   int nw = 4, cpw = 1;
-  att_b1_shape(x, max_len, &nw, &cpw);
+  if (R == 1)
+    att_b1_shape(x, max_len, &nw, &cpw);
+  else
+    att_batch_shape(x, R, max_len, &nw, &cpw);
   return nw;
 }
 
@@ -1413,6 +1444,12 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "rows_merge") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "rows_merge must be 0 or 1");
     x->rows_merge = value;
+  } else if (k == "gemv_balance") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "gemv_balance must be 0 or 1");
+    x->gemv_balance = value;
+  } else if (k == "att_nw6") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "att_nw6 must be 0 or 1");
+    x->att_nw6 = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
     if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;

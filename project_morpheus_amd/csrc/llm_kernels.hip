@@ -12,6 +12,8 @@
 #include "mx_common.h"
 #include "mx_llm_kernels.h"
 
+#include <initializer_list>
+
 namespace mx {
 
 // ---------------------------------------------------------------------------------
@@ -1015,14 +1017,38 @@ static int gemv_blocks(int N, int rpw, int ytiles, int target) {
   return b < cap ? b : (cap > 0 ? cap : 1);
 }
 
+// Option gemv_balance (GemvArgs::gemv_cus = the CU count): the waves per block whose grid puts
+// the fewest waves -- i.e. weight bytes -- on the most loaded CU.  A one-row GEMV streams each
+// CU's share at the CU's own fetch rate (MI355X_MICROARCH.md: prologue burst ~11 B/cycle/CU),
+// so a grid of 640 blocks on 256 CUs (2 or 3 blocks per CU) runs as long as 3 blocks.
+static int gemv_wpb_balanced(int G, int cus, std::initializer_list<int> cand) {
+  int best = 0, best_w = 1 << 30;
+  for (int w : cand) {
+    const int blocks = (G + w - 1) / w;
+    const int per_cu = (blocks + cus - 1) / cus * w;
+    if (per_cu < best_w) {
+      best = w;
+      best_w = per_cu;
+    }
+  }
+  return best;
+}
+
 template <int KCH, int RPW, int EPI, bool NORM, bool F8>
 static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
   const int G = a.N / RPW;
   if constexpr (EPI == EPI_RESID && !NORM && (F8 ? (KCH == 1 || KCH == 3)
                                                  : (KCH == 1 || KCH == 2 || KCH == 6))) {
-    if (a.att_ml) {  // R = 1 o-projection with the attention split merge (8-wave blocks)
+    if (a.att_ml) {  // R = 1 o-projection with the attention split merge (8- or 6-wave blocks)
       const int ns = a.att_nsm;
       if (ns > 8 || (KCH * 64 * (F8 ? 16 : 8)) / 8 > 512) return hipErrorInvalidValue;
+      if (a.gemv_cus > 0 && gemv_wpb_balanced(G, a.gemv_cus, {8, 6}) == 6) {
+        const dim3 grid((G + 5) / 6), blk(384);
+        if (ns <= 2) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 6, F8, 2>), grid, blk, 0, st, a);
+        else if (ns <= 4) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 6, F8, 4>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 6, F8, 8>), grid, blk, 0, st, a);
+        return hipGetLastError();
+      }
       const dim3 grid((G + 7) / 8), blk(512);
       if (ns <= 2) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8, 2>), grid, blk, 0, st, a);
       else if (ns <= 4) hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8, 4>), grid, blk, 0, st, a);
@@ -1031,6 +1057,12 @@ static hipError_t launch_gemv1_t(const GemvArgs& a, hipStream_t st) {
     }
   }
   if (a.att_ml) return hipErrorNotSupported;
+  if constexpr (EPI == EPI_QKV) {
+    if (a.gemv_cus > 0 && gemv_wpb_balanced(G, a.gemv_cus, {4, 5, 8}) == 5) {
+      hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 5, F8>), dim3((G + 4) / 5), dim3(320), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   if (a.wpb == 8)
     hipLaunchKernelGGL((gemv1_kernel<KCH, RPW, EPI, NORM, 8, F8>), dim3((G + 7) / 8), dim3(512), 0, st, a);
   else
@@ -1132,7 +1164,7 @@ hipError_t gemv_prepare(int kmax) {
 }
 
 hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t st) {
-  const int nw = a.nw == 8 ? 8 : 4;
+  const int nw = a.nw == 8 ? 8 : a.nw == 6 ? 6 : 4;
   const int S = 32 * nw * a.cpw;
   const int nsplit = (max_len + S - 1) / S;
   if (nsplit > ATT_MAX_SPLITS || (a.max_pos + S - 1) / S > a.split_stride || a.max_pos % 8)
@@ -1144,6 +1176,7 @@ hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t s
     return hipGetLastError();                                                        \
   }
 #define MX_ATG(G_) MX_AT(G_, 1, 4) MX_AT(G_, 2, 4) MX_AT(G_, 4, 4) \
+                   MX_AT(G_, 1, 6) MX_AT(G_, 2, 6) MX_AT(G_, 3, 6) \
                    MX_AT(G_, 1, 8) MX_AT(G_, 2, 8) MX_AT(G_, 3, 8) MX_AT(G_, 4, 8) \
                    MX_AT(G_, 6, 8) MX_AT(G_, 8, 8)
   MX_ATG(1) MX_ATG(2) MX_ATG(3) MX_ATG(4)

@@ -30,6 +30,8 @@ struct GemvArgs {
   int max_blocks;          // grid cap (0 = default)
   int force_legacy;        // 1: use the grid-stride kernel even for R = 1 (A/B timing)
   int wpb;                 // R = 1 kernel: waves per block (4 or 8; 0 = 8)
+  int gemv_cus;            // R = 1 kernel, option gemv_balance: CU count to balance the qkv /
+                           // merging o-proj grids over (0 = off)
   int rpw;                 // R = 1 kernel: weight rows per wave (0 = default per epilogue)
   float* ws;               // R >= 2 kernel: split-K partial tiles (gemm_rows_workspace)
   size_t ws_floats;

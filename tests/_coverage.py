@@ -38,6 +38,8 @@ GPU_RUNS = {
         [_r(ORPHEUS, [18], 24)],
     "test_gpu_llm.py::test_decode_parity_orpheus_width_no_o_merge":
         [_r(ORPHEUS, [18], 12, o_merge=0)],
+    **{f"test_gpu_llm.py::test_decode_parity_orpheus_width_no_gemv_balance[{p}]":
+       [_r(ORPHEUS_16K, [p], 16, gemv_balance=0)] for p in (200, 300, 600)},
     "test_gpu_llm.py::test_lm_head_grid_stride_orpheus_width":
         [_r(ORPHEUS, [24], 16, head_b1=0)],
     "test_gpu_llm.py::test_full_depth_orpheus_3b_single_stream":
@@ -70,13 +72,17 @@ GPU_RUNS = {
     **{f"test_gpu_llm.py::test_batched_decode_orpheus_width_32_rows_attention_chunks[{p}]":
        [_r(ORPHEUS_16K, [p + 5 + r for r in range(32)], 6)] for p in (280, 560, 850)},
     "test_gpu_llm.py::test_rows_merge_straddling_splits_orpheus_width[nsm2]":
-        [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12)],
+        [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, att_nw6=0)],
     "test_gpu_llm.py::test_rows_merge_straddling_splits_orpheus_width[nsm4]":
-        [_r(ORPHEUS_16K, [200, 260, 330, 480, 520, 600, 700, 760], 12)],
+        [_r(ORPHEUS_16K, [200, 260, 330, 480, 520, 600, 700, 760], 12, att_nw6=0)],
     "test_gpu_llm.py::test_batched_decode_orpheus_width_8_rows_split_attention[0]":
         [_r(ORPHEUS_16K, [520 + 3 + 5 * r for r in range(8)], 8, rows_merge=0)],
     "test_gpu_llm.py::test_batched_decode_orpheus_width_8_rows_split_attention[1]":
         [_r(ORPHEUS_16K, [520 + 3 + 5 * r for r in range(8)], 8, rows_merge=1)],
+    **{f"test_gpu_llm.py::test_batched_decode_orpheus_width_8_rows_six_wave_attention[{p}]":
+       [_r(ORPHEUS_16K, [p + 3 + 9 * r for r in range(8)], 6)] for p in (520, 1100)},
+    "test_gpu_llm.py::test_batched_decode_orpheus_width_8_rows_eight_wave_attention":
+        [_r(ORPHEUS_16K, [520 + 3 + 9 * r for r in range(8)], 6, att_nw6=0)],
     # ---- fp8 (e4m3 weights) -----------------------------------------------------------
     "test_gpu_fp8.py::test_fp8_single_stream_orpheus_width":
         [_r(ORPHEUS, [120], 16, f8=True)],
@@ -84,6 +90,8 @@ GPU_RUNS = {
         [_r(ORPHEUS, [5 + 4 * i for i in range(8)], 6, f8=True)],
     "test_gpu_fp8.py::test_fp8_batched_orpheus_width_8_rows_split_k_seam":
         [_r(ORPHEUS, [5 + 4 * i for i in range(8)], 6, f8=True, rows_atomic=0, rows_qkv_parts=0)],
+    "test_gpu_fp8.py::test_fp8_single_stream_orpheus_width_no_gemv_balance":
+        [_r(ORPHEUS_16K, [600], 16, f8=True, gemv_balance=0)],
     "test_gpu_fp8.py::test_fp8_lm_head_grid_stride_orpheus_width":
         [_r(ORPHEUS, [40], 12, f8=True, head_b1=0)],
     "test_gpu_fp8.py::test_fp8_batched_orpheus_width_8_rows_split_attention_merged_in_oproj":
@@ -93,9 +101,9 @@ GPU_RUNS = {
     "test_gpu_fp8.py::test_fp8_one_row_orpheus_width_split_classes":
         [_r(ORPHEUS_16K, [250], 16, f8=True)],
     "test_gpu_fp8.py::test_fp8_rows_merge_straddling_splits_orpheus_width[nsm2]":
-        [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, f8=True)],
+        [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, f8=True, att_nw6=0)],
     "test_gpu_fp8.py::test_fp8_rows_merge_straddling_splits_orpheus_width[nsm4]":
-        [_r(ORPHEUS_16K, [200, 260, 330, 480, 520, 600, 700, 760], 12, f8=True)],
+        [_r(ORPHEUS_16K, [200, 260, 330, 480, 520, 600, 700, 760], 12, f8=True, att_nw6=0)],
     # ---- the persistent one-row engine (option b1_engine) ----------------------------
     "test_gpu_engine_b1.py::test_engine_orpheus_width[bf16]":
         [_r(ORPHEUS_16K, [600], 40, b1_engine=1)],

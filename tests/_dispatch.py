@@ -47,7 +47,7 @@ DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
                 rows_nt_max=0, rows_nt1=2, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
                 rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7, rows_atomic=1,
-                rows_qkv_parts=1)
+                rows_qkv_parts=1, att_nw6=1, gemv_balance=1)
 # (rows_atomic and rows_qkv_parts select the residual projections' split-K epilogue at run time inside the same
 # instantiation -- float atomics into h / raw partials summed by the attention, or the
 # seam -- so they change no kernel key)
@@ -87,7 +87,12 @@ def att_shape(d, R, max_len, o):
             pairs = R * d.kv_heads
             splits = 1 if pairs > 64 else max(1, 256 // pairs)
             chunks = (max_len + 31) // 32
-            cpw = att_cpw_pick((chunks + splits * nw - 1) // (splits * nw), nw)
+            if o.get("att_nw6", 0) and splits > 1:  # capi.hip att_batch_shape
+                for nw, cpw in ((6, 1), (8, 1), (6, 2), (8, 2), (6, 3), (8, 3), (8, 4), (8, 6), (8, 8)):
+                    if (chunks + nw * cpw - 1) // (nw * cpw) <= splits:
+                        break
+            else:
+                cpw = att_cpw_pick((chunks + splits * nw - 1) // (splits * nw), nw)
     S = 32 * nw * cpw
     return nw, cpw, (max_len + S - 1) // S
 
@@ -185,12 +190,30 @@ def gemv1_launch(N, K, epi, norm, f8, o, rpw=0, nsm=0):
           (4, EPI_SILU, True), (1, EPI_STORE, False), (1, EPI_STORE, True)}
     if kch not in (1, 2, 3, 4, 6, 8, 16) or (rpw, epi, norm) not in ok or N % rpw:
         return None
+    G = N // rpw
     if nsm:
         if not (kch in ((1, 3) if f8 else (1, 2, 6)) and epi == EPI_RESID and not norm):
             raise ValueError("the merging o-proj has no instantiation for this width")
         m = 2 if nsm <= 2 else 4 if nsm <= 4 else 8
-        return f"gemv1_kernel<{kch}, {rpw}, {epi}, {_b(norm)}, 8, {_b(f8)}, {m}>"
-    return f"gemv1_kernel<{kch}, {rpw}, {epi}, {_b(norm)}, {o['gemv_wpb']}, {_b(f8)}, 0>"
+        wpb = 6 if o.get("gemv_balance", 0) and gemv_wpb_balanced(G, (8, 6)) == 6 else 8
+        return f"gemv1_kernel<{kch}, {rpw}, {epi}, {_b(norm)}, {wpb}, {_b(f8)}, {m}>"
+    wpb = o["gemv_wpb"]
+    if epi == EPI_QKV and o.get("gemv_balance", 0) and gemv_wpb_balanced(G, (4, 5, 8)) == 5:
+        wpb = 5
+    return f"gemv1_kernel<{kch}, {rpw}, {epi}, {_b(norm)}, {wpb}, {_b(f8)}, 0>"
+
+
+CUS = 256  # MI355X compute units (option gemv_balance queries the device)
+
+
+def gemv_wpb_balanced(G, cand):
+    """llm_kernels.hip gemv_wpb_balanced: fewest waves on the most loaded CU, first wins ties."""
+    best, best_w = 0, 1 << 30
+    for w in cand:
+        per_cu = -(-(-(-G // w)) // CUS) * w
+        if per_cu < best_w:
+            best, best_w = w, per_cu
+    return best
 
 
 def gemv_launch(N, K, R, epi, norm, f8, o, rpw=0, nsm=0, kind=None):

@@ -98,6 +98,17 @@ def test_fp8_single_stream_orpheus_width():
     assert _check(cfg, qw, [prompt], 16) >= 12
 
 
+def test_fp8_single_stream_orpheus_width_no_gemv_balance():
+    """Option gemv_balance = 0 with e4m3 weights: the one-row qkv GEMV on 4-wave blocks and the
+    merging o-proj on 8-wave blocks at 5 attention splits (NSM 8)."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    qw = quantize_fp8(synthetic_llm_weights(cfg, seed=92), cfg)
+    rng = np.random.default_rng(93)
+    prompt = [int(x) for x in rng.integers(0, cfg.vocab, 600)]
+    assert _check(cfg, qw, [prompt], 16, options={"gemv_balance": 0}, max_pos=1024,
+                  max_prefill=600) >= 12
+
+
 def test_fp8_batched_orpheus_width_8_rows():
     """configs[4] per GPU: 8 fp8 streams at Orpheus widths through the default multi-row GEMM
     with e4m3 weight tiles (converted in registers to bf16 MFMA fragments, per-row scales in
@@ -176,7 +187,8 @@ def test_fp8_one_row_orpheus_width_split_classes():
 def test_fp8_rows_merge_straddling_splits_orpheus_width(case):
     """configs[4]'s e4m3 merging o-projection (gemm_rows_kernel<1,1,1,false,3,true,2,NSM>)
     where the 8 rows of one launch have different split counts (1..2 under NSM 2, 1..4 under
-    NSM 4; the cases of test_gpu_llm.test_rows_merge_straddling_splits_orpheus_width)."""
+    NSM 4; the cases of test_gpu_llm.test_rows_merge_straddling_splits_orpheus_width, on the
+    256-position splits of 8-wave blocks: option att_nw6 = 0)."""
     lens, steps = STRADDLE[case]
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     qw = quantize_fp8(synthetic_llm_weights(cfg, seed=81 if case == "nsm2" else 82), cfg)
@@ -184,5 +196,5 @@ def test_fp8_rows_merge_straddling_splits_orpheus_width(case):
     prefix = [int(x) for x in rng.integers(0, cfg.vocab, 190)]
     prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, n - 190)] for n in lens]
     assert rows_teacher_forced(cfg, qw, prompts, steps, shared_prefix=190, max_pos=1024,
-                               max_prefill=768, wdtype="fp8",
-                               ref_w=dequantize_fp8(qw)) >= 0.8 * 8 * steps
+                               max_prefill=768, wdtype="fp8", ref_w=dequantize_fp8(qw),
+                               options={"att_nw6": 0}) >= 0.8 * 8 * steps

@@ -213,9 +213,9 @@ def test_batched_decode_orpheus_width_32_rows_attention_chunks(prefix_len):
 @pytest.mark.parametrize("rows_merge", [0, 1])
 def test_batched_decode_orpheus_width_8_rows_split_attention(rows_merge):
     """configs[3]'s 8-GPU row class (8 rows per GPU) at a context where the multi-row attention
-    splits (a 520-id shared prefix + ragged tails: 3 splits of 256 positions per (row, kv
-    head)): rows_merge 0 merges the splits in the attention (ticket, last arriver), 1 in the
-    generation-4 o-projection's activation staging (attn no_merge)."""
+    splits (a 520-id shared prefix + ragged tails: 3 splits of 192 positions per (row, kv
+    head), 6-wave blocks): rows_merge 0 merges the splits in the attention (ticket, last
+    arriver), 1 in the generation-4 o-projection's activation staging (attn no_merge)."""
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     w = synthetic_llm_weights(cfg, seed=18)
     rng = np.random.default_rng(19)
@@ -226,6 +226,39 @@ def test_batched_decode_orpheus_width_8_rows_split_attention(rows_merge):
                                max_prefill=576, options={"rows_merge": rows_merge}) >= 0.8 * 8 * steps
 
 
+@pytest.mark.parametrize("prefix_len", [520, 1100])
+def test_batched_decode_orpheus_width_8_rows_six_wave_attention(prefix_len):
+    """The 8-row attention on 6-wave blocks (option att_nw6, the default): the shortest split
+    that covers the context in <= 4 splits (capi.hip att_batch_shape): attn_kernel<3,1,6>
+    (192-position splits) after a 520-id prefix, attn_kernel<3,2,6> (384) after 1,100, ragged
+    tails so that rows of one launch have different split counts; the o-projection merges
+    them (rows_merge)."""
+    from _dispatch import ORPHEUS_16K, att_shape, DEFAULTS
+    steps = 6
+    lens = [prefix_len + 3 + 9 * r for r in range(8)]
+    shapes = {att_shape(ORPHEUS_16K, 8, max(lens) + k, DEFAULTS)[:2] for k in range(1, steps)}
+    assert shapes == {(6, 1 if prefix_len == 520 else 2)}, shapes
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=80 + prefix_len)
+    rng = np.random.default_rng(81)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, prefix_len)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, n - prefix_len)] for n in lens]
+    assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=prefix_len, max_pos=1536,
+                               max_prefill=prefix_len + 80) >= 0.8 * 8 * steps
+
+
+def test_batched_decode_orpheus_width_8_rows_eight_wave_attention():
+    """Option att_nw6 = 0: the 8-row attention on 8-wave blocks only (3 splits of 256
+    positions after a 520-id prefix: attn_kernel<3,1,8>), merged in the o-projection."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=82)
+    rng = np.random.default_rng(83)
+    prefix = [int(x) for x in rng.integers(0, cfg.vocab, 520)]
+    prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, 3 + 9 * r)] for r in range(8)]
+    assert rows_teacher_forced(cfg, w, prompts, 6, shared_prefix=520, max_pos=1024,
+                               max_prefill=600, options={"att_nw6": 0}) >= 0.8 * 8 * 6
+
+
 @pytest.mark.parametrize("case", sorted(STRADDLE))
 def test_rows_merge_straddling_splits_orpheus_width(case):
     """The generation-4 merging o-projection (rows_merge, the default) where the rows of one
@@ -234,7 +267,8 @@ def test_rows_merge_straddling_splits_orpheus_width(case):
     partial loads and the s < ns skip of mx_rows_v4.inc row_merge_load / row_merge_apply."""
     from _dispatch import ORPHEUS_16K, att_shape, DEFAULTS
     lens, steps = STRADDLE[case]
-    nsm = {att_shape(ORPHEUS_16K, 8, max(lens) + k, DEFAULTS)[2] for k in range(1, steps)}
+    o = dict(DEFAULTS, att_nw6=0)  # the 256-position splits of 8-wave blocks
+    nsm = {att_shape(ORPHEUS_16K, 8, max(lens) + k, o)[2] for k in range(1, steps)}
     row_ns = {(n + k + 255) // 256 for n in lens for k in range(1, steps)}
     assert nsm == ({2} if case == "nsm2" else {3, 4}), nsm
     assert row_ns == ({1, 2} if case == "nsm2" else {1, 2, 3, 4}), row_ns
@@ -244,7 +278,7 @@ def test_rows_merge_straddling_splits_orpheus_width(case):
     prefix = [int(x) for x in rng.integers(0, cfg.vocab, 190)]
     prompts = [prefix + [int(x) for x in rng.integers(0, cfg.vocab, n - 190)] for n in lens]
     assert rows_teacher_forced(cfg, w, prompts, steps, shared_prefix=190, max_pos=1024,
-                               max_prefill=768) >= 0.8 * 8 * steps
+                               max_prefill=768, options={"att_nw6": 0}) >= 0.8 * 8 * steps
 
 
 def test_decode_parity_orpheus_width_2_layers():
@@ -264,6 +298,20 @@ def test_decode_parity_orpheus_width_no_o_merge():
     w = synthetic_llm_weights(cfg, seed=77)
     prompt = _orpheus_prompt(12, 78)
     assert _compare(cfg, w, prompt, 12, options={"o_merge": 0}) >= 9
+
+
+@pytest.mark.parametrize("prompt_len", [200, 300, 600])
+def test_decode_parity_orpheus_width_no_gemv_balance(prompt_len):
+    """Option gemv_balance = 0: the one-row qkv GEMV on 4-wave blocks (gemv1<6,2,3,true,4,...>,
+    640 blocks) and the merging o-proj on 8-wave blocks (192 blocks) at 2 / 3 / 5 attention
+    splits (NSM 2 / 4 / 8), 16 steps (the default balances them over the CUs: 5- and 6-wave
+    blocks)."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=90 + prompt_len)
+    rng = np.random.default_rng(91)
+    prompt = [int(x) for x in rng.integers(0, cfg.vocab, prompt_len)]
+    assert _compare(cfg, w, prompt, 16, options={"gemv_balance": 0}, max_pos=1024,
+                    max_prefill=prompt_len) >= 12
 
 
 def test_lm_head_grid_stride_orpheus_width():
