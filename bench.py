@@ -162,7 +162,8 @@ def rocprof_avg_us(kernel=ROOFLINE_KERNEL):
     import csv
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats*.csv")),
-                   key=lambda f: (os.path.basename(f)[:3], os.path.getmtime(f)))
+                   key=lambda f: (os.path.basename(f)[:3], "final" in os.path.basename(f),
+                                  os.path.getmtime(f)))
     for path in reversed(files):
         try:
             with open(path) as fh:
