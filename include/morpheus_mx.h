@@ -193,7 +193,8 @@ int mx_snac_finalize(mx_snac* ctx);
  * per window (device-accessible [batch], e.g. host-mapped; a window's noise then depends on
  * its own seed only) or, with seeds NULL, from `seed` over the whole batch.
  * pcm: [batch][hi-lo] int16 of samples [lo,hi) (NULL to skip); audio: [batch][2048*n_frames]
- * fp32 full window (NULL to skip). */
+ * fp32 full window (NULL to skip).  With audio NULL only the positions [lo,hi) depend on are
+ * computed past the first DecoderBlock (the same PCM within fp32 summation order). */
 int mx_snac_decode(mx_snac* ctx, const int32_t* frames, int n_frames, int batch,
                    const float* noise, uint64_t seed, const uint64_t* seeds, int16_t* pcm,
                    float* audio, int lo, int hi, void* stream);

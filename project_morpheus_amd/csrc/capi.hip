@@ -1588,11 +1588,12 @@ struct mx_snac {
   uint16_t* up_bf[4][8] = {};
   int up_delta[4][8][2] = {};
   float *bufA = nullptr, *bufB = nullptr, *bufC = nullptr, *noise = nullptr;
+  float* bufD = nullptr;  // block 0's Snake output cut to the kept slice's receptive field
   size_t buf_elems = 0;
   bool final = false;
   SnacIO* io = nullptr;  // device copy of the per-call pointers read by captured windows
   hipStream_t cap = nullptr;  // capture stream (the caller's may be the null stream)
-  std::map<std::array<int, 4>, hipGraphExec_t> graphs;  // (n_frames, batch, lo, hi)
+  std::map<std::array<int, 5>, hipGraphExec_t> graphs;  // (n_frames, batch, lo, hi, pcm only)
   std::vector<hipGraph_t> graph_defs;
 };
 
@@ -1647,7 +1648,8 @@ extern "C" int mx_snac_create(int device, int max_frames, int max_batch, mx_snac
   if (e == hipSuccess) { s->allocs.push_back(p); s->bufA = (float*)p; e = hipMalloc(&p, s->buf_elems * 4); }
   if (e == hipSuccess) { s->allocs.push_back(p); s->bufB = (float*)p; e = hipMalloc(&p, s->buf_elems * 4); }
   if (e == hipSuccess) { s->allocs.push_back(p); s->bufC = (float*)p; e = hipMalloc(&p, (size_t)3360 * max_frames * max_batch * 4); }
-  if (e == hipSuccess) { s->allocs.push_back(p); s->noise = (float*)p; e = hipMalloc(&p, sizeof(SnacIO)); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->noise = (float*)p; e = hipMalloc(&p, (size_t)16384 * max_frames * max_batch * 4); }
+  if (e == hipSuccess) { s->allocs.push_back(p); s->bufD = (float*)p; e = hipMalloc(&p, sizeof(SnacIO)); }
   if (e == hipSuccess) { s->allocs.push_back(p); s->io = (SnacIO*)p; }
   if (e != hipSuccess) {
     g_err = std::string("snac alloc failed: ") + hipGetErrorString(e);
@@ -1772,10 +1774,36 @@ static void pick_tiles(ConvGemmArgs& g, int nphase) {
     g.wk *= 2;
 }
 
+// Receptive-field cut of a PCM-only window decode (round 6): the kept samples [lo, hi) of a
+// window depend on block 0's output positions [c0, c1) only (the output conv's 7 taps, each
+// block's three residual units -- dilations 1, 3, 9, 7 taps: 39 positions either side -- and its
+// ConvTranspose1d(k = 2s, stride s, pad ceil(s / 2)), whose output o reads the inputs i with
+// 0 <= o + pad - i s < 2s), plus one position of margin.  Blocks 1-3 then run on that range
+// alone (origins 8 c0, 32 c0, 64 c0): a zero at the cut edges stands where the full window has
+// values, but no position the kept slice reads depends on one.  [0, 32 n) when nothing is cut.
+static void snac_cut(int n_frames, int lo, int hi, int* c0, int* c1) {
+  const int T1 = 32 * n_frames;
+  *c0 = 0;
+  *c1 = T1;
+  if (hi <= lo) return;
+  auto fdiv = [](int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+  int L = lo - 3, H = hi + 3;  // Snake(block 3 output) positions the output conv reads: [L, H)
+  for (int b = 3; b >= 1; --b) {
+    L -= 3 * (kDil[0] + kDil[1] + kDil[2]);
+    H += 3 * (kDil[0] + kDil[1] + kDil[2]);
+    const int st = kRates[b], pad = (st + 1) / 2;
+    L = -fdiv(-(L + pad - 2 * st + 1), st);  // ceil
+    H = fdiv(H - 1 + pad, st) + 1;
+  }
+  *c0 = std::max(0, L - 1);
+  *c1 = std::min(T1, H + 1);
+}
+
 // Every launch of one window decode (io != null: the pointers come from s->io at run time).
 static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int batch,
                         const float* noise, uint64_t seed, const uint64_t* seeds, int16_t* pcm,
-                        float* audio, int lo, int hi, hipStream_t st, const SnacIO* io) {
+                        float* audio, int lo, int hi, hipStream_t st, const SnacIO* io,
+                        bool pcm_only) {
   auto W = [&](const std::string& n) { return s->w[n]; };
   auto WB = [&](const std::string& n) -> const uint16_t* { return s->wbf.at(n); };
   const int B = batch;
@@ -1801,11 +1829,24 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
     pick_tiles(g, 1);
     MX_TRY(s, launch_conv_gemm(g, 1, st));                                      // A: [T][1024]
   }
-  int noff = 0;
+  // PCM-only calls run blocks 1-3 on the kept slice's receptive field (snac_cut); a call that
+  // also wants the whole window's audio runs them whole
+  int c0 = 0, c1 = 32 * n_frames;
+  if (pcm_only) snac_cut(n_frames, lo, hi, &c0, &c1);
+  const bool cut = c1 - c0 < 32 * n_frames;
+  int noff = 0, org = 0;  // noise offset of the block (full-window layout), cut origin
   for (int b = 0; b < 4; ++b) {
     const int cin = 1024 >> b, cout = cin / 2, sr = kRates[b];
     const std::string p = "b" + std::to_string(b) + ".";
+    const float* Xin = Cs;
+    if (b == 1 && cut) {  // block 0's Snake output, positions [c0, c1) of each window
+      MX_TRY(s, launch_snac_cut(Cs, s->bufD, B, T, cin, c0, c1 - c0, st));
+      Xin = s->bufD;
+      T = c1 - c0;
+      org = c0;
+    }
     const int To = T * sr;
+    org *= sr;
     {  // ConvTranspose1d on Snake(x): all sr phases in one launch, Cs [T][cin] -> Bf [To][cout]
       ConvGemmArgs g{};
       for (int ph = 0; ph < sr; ++ph) {
@@ -1813,7 +1854,7 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
         g.dph[ph][0] = s->up_delta[b][ph][0];
         g.dph[ph][1] = s->up_delta[b][ph][1];
       }
-      g.X = Cs; g.bias = W(p + "up.b"); g.out = Bf; g.M = cout; g.Cin = cin; g.Tin = T;
+      g.X = Xin; g.bias = W(p + "up.b"); g.out = Bf; g.M = cout; g.Cin = cin; g.Tin = T;
       g.Tout = To; g.B = B; g.nseg = 2; g.col_stride = sr; g.epi = CG_STORE;
       pick_tiles(g, sr);
       MX_TRY(s, launch_conv_gemm(g, sr, st));
@@ -1821,13 +1862,14 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
     T = To;
     {  // NoiseBlock: A = Bf + noise * (Wn Bf)
       ConvGemmArgs g{};
-      g.Abf[0] = WB(p + "noise.w"); g.X = Bf; g.R = Bf; g.noise = nz + noff; g.noise_stride = nlen;
+      g.Abf[0] = WB(p + "noise.w"); g.X = Bf; g.R = Bf; g.noise = nz + noff + org;
+      g.noise_stride = nlen;
       g.out = A; g.M = cout; g.Cin = cout; g.Tin = T; g.Tout = T; g.B = B; g.nseg = 1;
       g.col_stride = 1; g.epi = CG_NOISE;
       pick_tiles(g, 1);
       MX_TRY(s, launch_conv_gemm(g, 1, st));
     }
-    noff += T;
+    noff += 4 * n_frames * (b == 0 ? 8 : b == 1 ? 64 : b == 2 ? 256 : 512);  // full block output
     for (int r = 0; r < 3; ++r) {  // ResidualUnit(d): A += pw(Snake(dw_d(Snake(A))))
       const std::string q = p + "r" + std::to_string(r) + ".";
       MX_TRY(s, launch_dwconv(A, Bf, W(q + "dw.w"), W(q + "dw.b"), W(q + "alpha1"),
@@ -1844,8 +1886,8 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
       MX_TRY(s, launch_conv_gemm(g, 1, st));
     }
   }
-  MX_TRY(s, launch_snac_out(Cs, W("out.conv.w"), W("out.conv.b"), B, T, lo, hi, audio, pcm, st,
-                            io));
+  MX_TRY(s, launch_snac_out(Cs, W("out.conv.w"), W("out.conv.b"), B, T, lo - org, hi - org,
+                            audio, pcm, st, io));
   return MX_OK;
 }
 
@@ -1866,16 +1908,18 @@ extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, i
   if (lo > hi) lo = hi;
   hipStream_t st = (hipStream_t)stream;
   MX_TRY(s, hipSetDevice(s->device));
+  // (a call that wants the whole window's audio runs every position: snac_cut)
+  const bool pcm_only = pcm && !audio;
   if (noise) return snac_enqueue(s, frames, n_frames, batch, noise, seed, seeds, pcm, audio, lo,
-                                 hi, st, nullptr);
-  const std::array<int, 4> key{n_frames, batch, lo, hi};
+                                 hi, st, nullptr, pcm_only);
+  const std::array<int, 5> key{n_frames, batch, lo, hi, pcm_only ? 1 : 0};
   auto it = s->graphs.find(key);
   if (it == s->graphs.end()) {
     hipGraph_t g = nullptr;
     if (!s->cap) MX_TRY(s, hipStreamCreateWithFlags(&s->cap, hipStreamNonBlocking));
     MX_TRY(s, hipStreamBeginCapture(s->cap, hipStreamCaptureModeRelaxed));
     const int rc = snac_enqueue(s, nullptr, n_frames, batch, nullptr, 0, nullptr, nullptr,
-                                nullptr, lo, hi, s->cap, s->io);
+                                nullptr, lo, hi, s->cap, s->io, pcm_only);
     hipError_t e2 = hipStreamEndCapture(s->cap, &g);
     if (rc != MX_OK) {
       if (g) (void)hipGraphDestroy(g);

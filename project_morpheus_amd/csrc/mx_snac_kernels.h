@@ -53,5 +53,7 @@ hipError_t launch_split_planes(const float* src, uint16_t* dst, int64_t n, hipSt
 hipError_t launch_snac_out(const float* xs, const float* w, const float* b, int B, int T,
                            int lo, int hi, float* audio, int16_t* pcm, hipStream_t st,
                            const SnacIO* io = nullptr);
+hipError_t launch_snac_cut(const float* src, float* dst, int B, int T, int C, int c0, int n,
+                           hipStream_t st);
 
 }  // namespace mx

@@ -125,14 +125,19 @@ SNAC_RUNS = {
        for n, b in ((1, 1), (4, 1), (7, 1), (7, 3), (2, 2), (1, 5), (4, 9), (7, 12), (5, 1),
                     (5, 12))},
     "test_gpu_snac.py::test_snac_batched_32_windows_matches_oracle": [(7, 32)],
+    # PCM-only calls: blocks 1-3 on the kept slice's receptive field (capi.hip snac_cut)
+    **{f"test_gpu_snac.py::test_snac_cut_pcm_parity[{n}-{b}]": [(n, b, True)]
+       for n, b in ((5, 1), (4, 5), (5, 12), (5, 32))},
 }
 
 
-def check_declared_snac(n_frames, batch):
+def check_declared_snac(n_frames, batch, cut=False):
+    """cut: a PCM-only call with the serving slice (blocks 1-3 cut to its receptive field)."""
     node = current_test()
     runs = SNAC_RUNS.get(node)
     assert runs is not None, f"{node}: SNAC GPU run not declared in tests/_coverage.py"
-    assert (n_frames, batch) in runs, f"{node}: ({n_frames}, {batch}) is not declared ({runs})"
+    run = (n_frames, batch, True) if cut else (n_frames, batch)
+    assert run in runs, f"{node}: {run} is not declared ({runs})"
 
 
 def current_test():

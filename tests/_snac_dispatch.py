@@ -62,13 +62,37 @@ def name_of(key):
     return key.split(" [")[0]
 
 
-def window_keys(n_frames, B):
-    """Every kernel key of one mx_snac_decode call of B windows of n_frames frames."""
+def snac_cut(n_frames, lo, hi):
+    """capi.hip snac_cut: block 0's output positions [c0, c1) the kept samples [lo, hi) depend on
+    (output conv 7 taps; per block three residual units of 7 taps at dilations 1, 3, 9 and the
+    ConvTranspose1d(k = 2s, stride s, pad ceil(s / 2))), one position of margin."""
+    T1 = 32 * n_frames
+    if hi <= lo:
+        return 0, T1
+    L, H = lo - 3, hi + 3
+    for b in (3, 2, 1):
+        L -= 3 * sum(K_DIL)
+        H += 3 * sum(K_DIL)
+        st = K_RATES[b]
+        pad = (st + 1) // 2
+        L = -((-(L + pad - 2 * st + 1)) // st)
+        H = (H - 1 + pad) // st + 1
+    return max(0, L - 1), min(T1, H + 1)
+
+
+def window_keys(n_frames, B, lo=None, hi=None):
+    """Every kernel key of one mx_snac_decode call of B windows of n_frames frames; with the
+    kept slice [lo, hi) of a PCM-only call (the serving path), blocks 1-3 run on its receptive
+    field (capi.hip snac_cut)."""
     T = 4 * n_frames
+    c0, c1 = (0, 32 * n_frames) if lo is None else snac_cut(n_frames, lo, hi)
     keys = {"snac_embed_kernel", dwconv_key(B, T), conv_gemm_key(1024, 768, T, B, 1, 1)}
     for b in range(4):
         cin = 1024 >> b
         cout, sr = cin // 2, K_RATES[b]
+        if b == 1 and c1 - c0 < T:
+            keys.add("snac_cut_kernel")
+            T = c1 - c0
         keys.add(conv_gemm_key(cout, cin, T, B, 2, sr))   # polyphase ConvTranspose (all phases)
         T *= sr
         keys.add(conv_gemm_key(cout, cout, T, B, 1, 1))   # NoiseBlock
@@ -86,9 +110,19 @@ def window_keys(n_frames, B):
 SERVING_FRAMES = (1, 4, 5)
 
 
-def envelope(max_batch=32, frames=SERVING_FRAMES):
+SLICE_LO, SLICE_HI = 2048, 4096  # speechpipe.py:122
+
+
+def serving_slice(n):
+    """engine.SnacDecoder.decode's slice of an n-frame window (clamped to the window)."""
+    hi = min(SLICE_HI, 2048 * n)
+    return min(SLICE_LO, hi), hi
+
+
+def envelope(max_batch=32, frames=SERVING_FRAMES, cut=True):
+    """cut=False: the library before snac_cut (round 6), for the traces recorded with it."""
     keys = set()
     for n in frames:
         for B in range(1, max_batch + 1):
-            keys |= window_keys(n, B)
+            keys |= window_keys(n, B, *serving_slice(n)) if cut else window_keys(n, B)
     return keys

@@ -15,6 +15,13 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+def snac_pair_32():
+    from project_morpheus_amd.engine import SnacDecoder
+    w = synthetic_snac_weights(seed=3)
+    return w, SnacDecoder(w, device=0, max_frames=7, max_batch=32)
+
+
+@pytest.fixture(scope="module")
 def snac_pair():
     from project_morpheus_amd.engine import SnacDecoder
     w = synthetic_snac_weights(seed=3)
@@ -66,6 +73,34 @@ def test_snac_window_parity(snac_pair, n_frames, B):
         assert pcm[b].shape == ref_pcm.shape
         if ref_pcm.size:  # a 1-frame window's [2048:4096] slice is empty (speechpipe.py:122)
             assert np.abs(pcm[b].astype(np.int32) - ref_pcm).max() <= 1
+
+
+@pytest.mark.parametrize("n_frames,B", [(5, 1), (4, 5), (5, 12), (5, 32)])
+def test_snac_cut_pcm_parity(snac_pair_32, n_frames, B):
+    """PCM-only calls (the serving path) run blocks 1-3 on the kept samples' receptive field
+    (capi.hip snac_cut, tests/test_oracle_snac.py): their PCM against the WHOLE-window oracle,
+    within 1 LSB, for single windows, a 5-window batch (one-wave conv-GEMMs, ragged tiles) and
+    12 / 32-window batches (the block-tiled conv-GEMM)."""
+    from _coverage import check_declared_snac
+    check_declared_snac(n_frames, B, cut=True)
+    w, dec = snac_pair_32
+    rng = np.random.default_rng(200 + n_frames + B)
+    codes = rng.integers(0, 4096, size=(B, 7 * n_frames)).astype(np.int32)
+    noise = _noise(B, n_frames, 9 + n_frames)
+    pcm, audio = dec.decode(torch.from_numpy(codes).cuda(), noise=noise.cuda(), want_audio=False)
+    torch.cuda.synchronize()
+    assert audio is None
+    pcm = pcm.cpu().numpy()
+    hi = min(4096, 2048 * n_frames)
+    for b in range(0, B, 1 if B <= 5 else 5):
+        c = codes[b].tolist()
+        c0 = [c[7 * f] for f in range(n_frames)]
+        c1 = [c[7 * f + j] for f in range(n_frames) for j in (1, 4)]
+        c2 = [c[7 * f + j] for f in range(n_frames) for j in (2, 3, 5, 6)]
+        want = snac_ref.decode(w, c0, c1, c2, noise=_split_noise(noise[b], n_frames))
+        ref_pcm = (want.reshape(-1).numpy()[2048:hi] * np.float32(32767)).astype(np.int16)
+        assert pcm[b].shape == ref_pcm.shape
+        assert np.abs(pcm[b].astype(np.int32) - ref_pcm).max() <= 1, b
 
 
 def test_snac_audio_is_nontrivial(snac_pair):

@@ -99,3 +99,70 @@ def test_kept_slice_depends_on_the_first_five_frames_only():
     short = _decode_window(w, codes[: 7 * n], n, snac_ref.window_noise(11, n))[2048:4096]
     d = (short - full).abs()
     assert float(d.max()) < 2e-5 and float(d.pow(2).mean().sqrt()) < 5e-6
+
+
+def _decode_cut(w, codes, n, noise, lo, hi, cut=None, poke=None):
+    """The library's PCM-only decode (capi.hip snac_enqueue with snac_cut): input stage and
+    block 0 whole, then blocks 1-3 and the output conv on block 0's positions [c0, c1) only,
+    zero-padded at the cut edges, noise taken at the cut's origin; returns samples [lo, hi).
+    cut=(0, 32 n) is the whole-window decode; poke=q adds 1 to block 0's Snake output at q."""
+    from _snac_dispatch import snac_cut
+    c0, c1 = cut if cut is not None else snac_cut(n, lo, hi)
+    p = w
+    cc = [codes[7 * f] for f in range(n)]
+    c1c = [codes[7 * f + j] for f in range(n) for j in (1, 4)]
+    c2c = [codes[7 * f + j] for f in range(n) for j in (2, 3, 5, 6)]
+    with torch.no_grad():
+        z = snac_ref.from_codes(p, [torch.as_tensor(c).reshape(1, -1) for c in (cc, c1c, c2c)])
+        x = F.conv1d(z, p["in.dw.w"], p["in.dw.b"], padding=3, groups=z.shape[1])
+        x = F.conv1d(x, p["in.pw.w"].unsqueeze(-1), p["in.pw.b"])
+        org = 0
+        for b, st in enumerate(snac_ref.RATES):
+            x = snac_ref.snake(x, p[f"b{b}.alpha"])
+            if b == 1:
+                if poke is not None:
+                    x = x.clone()
+                    x[:, :, poke] += 1.0
+                x, org = x[:, :, c0:c1], c0
+            org *= st
+            x = F.conv_transpose1d(x, p[f"b{b}.up.w"], p[f"b{b}.up.b"], stride=st,
+                                   padding=math.ceil(st / 2), output_padding=st % 2)
+            h = F.conv1d(x, p[f"b{b}.noise.w"].unsqueeze(-1))
+            x = x + noise[b][:, :, org:org + x.shape[2]] * h
+            for r, d in enumerate(snac_ref.DILATIONS):
+                y = snac_ref.snake(x, p[f"b{b}.r{r}.alpha1"])
+                y = F.conv1d(y, p[f"b{b}.r{r}.dw.w"], p[f"b{b}.r{r}.dw.b"], padding=3 * d,
+                             dilation=d, groups=x.shape[1])
+                y = snac_ref.snake(y, p[f"b{b}.r{r}.alpha2"])
+                x = x + F.conv1d(y, p[f"b{b}.r{r}.pw.w"].unsqueeze(-1), p[f"b{b}.r{r}.pw.b"])
+        x = snac_ref.snake(x, p["out.alpha"])
+        x = torch.tanh(F.conv1d(x, p["out.conv.w"], p["out.conv.b"], padding=3)).reshape(-1)
+    return x[lo - org:hi - org]
+
+
+@pytest.mark.parametrize("n", [4, 5, 7])
+def test_receptive_field_cut_keeps_the_kept_samples(n):
+    """capi.hip snac_cut: a PCM-only call runs blocks 1-3 on the kept samples' receptive field
+    in block 0's output (50 of 32 N positions for [2048, 4096), one of them margin on either
+    side).  The cone is exact: a change to block 0's output just outside it leaves the kept
+    samples of the whole-window decode bit-identical, one at its edge changes them; and the cut
+    decode gives the kept samples within fp32 summation order (torch's conv algorithms vary
+    with the length)."""
+    import numpy as np
+
+    from _snac_dispatch import serving_slice, snac_cut
+    w = synthetic_snac_weights(seed=3)
+    codes = [int(v) for v in np.random.default_rng(n).integers(0, 4096, 7 * n)]
+    noise = snac_ref.window_noise(17, n)
+    lo, hi = serving_slice(n)
+    c0, c1 = snac_cut(n, lo, hi)
+    assert (c0, c1) == (23, 73)
+    whole = (0, 32 * n)
+    full = _decode_cut(w, codes, n, noise, lo, hi, cut=whole)
+    assert torch.equal(full, _decode_window(w, codes, n, noise)[lo:hi])
+    for q in (c0, c1 - 1):  # the margin positions: outside the cone
+        assert torch.equal(_decode_cut(w, codes, n, noise, lo, hi, cut=whole, poke=q), full)
+    for q in (c0 + 1, c1 - 2):  # the cone's edges
+        assert not torch.equal(_decode_cut(w, codes, n, noise, lo, hi, cut=whole, poke=q), full)
+    d = (_decode_cut(w, codes, n, noise, lo, hi) - full).abs()
+    assert float(d.max()) < 1e-5 and float(d.pow(2).mean().sqrt()) < 2e-6, float(d.max())
