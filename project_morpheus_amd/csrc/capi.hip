@@ -1891,8 +1891,9 @@ static int snac_enqueue(mx_snac* s, const int32_t* frames, int n_frames, int bat
   return MX_OK;
 }
 
-// One window batch.  Device-drawn noise (noise == NULL, the serving path): the 36 launches
-// are captured once per (n_frames, batch, slice) into a hipGraph and replayed after a 1-thread
+// One window batch.  Device-drawn noise (noise == NULL, the serving path): the 36 launches (37
+// with the receptive-field cut) are captured once per (n_frames, batch, slice, PCM only) into a
+// hipGraph and replayed after a 1-thread
 // kernel stores this call's pointers for the captured kernels to read.  Explicit noise (the
 // parity tests) runs eagerly.
 extern "C" int mx_snac_decode(mx_snac* s, const int32_t* frames, int n_frames, int batch,

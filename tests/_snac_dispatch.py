@@ -3,8 +3,8 @@
 A restatement of the library's SNAC dispatch, so that the parity tests' coverage of the
 kernels the bench runs can be checked on the CPU (tests/test_snac_coverage.py):
 
-* ``capi.hip`` ``snac_enqueue`` (the 36 launches of one call: embed, input depthwise conv and
-  1x1 conv, then per DecoderBlock the polyphase ConvTranspose, the NoiseBlock and three
+* ``capi.hip`` ``snac_enqueue`` (the 36 launches of one call, 37 with the receptive-field cut
+  of a PCM-only call: embed, input depthwise conv and 1x1 conv, then per DecoderBlock the polyphase ConvTranspose, the NoiseBlock and three
   ResidualUnits, then the output stage) and ``pick_tiles`` (block-tiled kernel from
   ``snac_tiled_min_batch()`` = 8 windows when M % 64 == 0; otherwise 16 x NSUB column tiles,
   NSUB = 4 from 2,048 input steps, and WK K-splitting waves doubled while the launch stays
