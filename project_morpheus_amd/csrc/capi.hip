@@ -687,8 +687,15 @@ static void attach_ws(mx_llm* x, GemvArgs& g) {
 // second read is served on-die in part).  Measured at 20-32 rows, L 300 / 900: qkv + o-proj +
 // down (mask 11, the default) 4-5 % per step; gate/up and the lm_head lose
 // (profiles/r05_rows_nt1.log)
+// Above 32 rows (prefill, 64-row decode) the layer launches take 32-row batch tiles when
+// rows_nt_max is 0 (auto) and the weights are e4m3 or the rows at most 128: measured per
+// prefill, bf16 48 / 64 ids 3.19 / 3.34 -> 2.75 / 2.77 ms, 128 equal, 256 / 512 slower
+// (8.03 -> 8.52 ms); e4m3 faster at every length (48 ids -20 %, 512 ids -5 %)
+// (profiles/r06_prefill_batch_tiles.log)
 static void nt_cap(const mx_llm* x, GemvArgs& g, int kind_bit, int R) {
   if ((x->rows_nt1 >> kind_bit) & 1 && R <= 32) g.rows_nt_max = 1;
+  else if (x->rows_nt_max == 0 && kind_bit < 4 && R > 32 && (x->c.wdtype == WT_FP8 || R <= 128))
+    g.rows_nt_max = 2;
   if (kind_bit < 4 && x->rows_target_k[kind_bit] > 0) g.rows_target = x->rows_target_k[kind_bit];
 }
 

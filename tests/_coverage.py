@@ -71,6 +71,8 @@ GPU_RUNS = {
         [_r(ORPHEUS_16K, [1400 + 5 + r for r in range(32)], 12)],
     **{f"test_gpu_llm.py::test_batched_decode_orpheus_width_32_rows_attention_chunks[{p}]":
        [_r(ORPHEUS_16K, [p + 5 + r for r in range(32)], 6)] for p in (280, 560, 850)},
+    "test_gpu_llm.py::test_prefill_batch_tile_classes_orpheus_width":
+        [_r(ORPHEUS_16K, [100, 150], 6)],
     "test_gpu_llm.py::test_rows_merge_straddling_splits_orpheus_width[nsm2]":
         [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, att_nw6=0)],
     "test_gpu_llm.py::test_rows_merge_straddling_splits_orpheus_width[nsm4]":

@@ -143,17 +143,21 @@ def target_opts(o, kind):
     return o
 
 
-def nt_max_of(o, kind, R):
+def nt_max_of(o, kind, R, f8=False):
     """capi.hip nt_cap: option rows_nt1 puts this kind's 17-32-row launches on 16-row tiles
-    (kind: 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head; None: not a layer launch)."""
+    (kind: 0 qkv, 1 o-proj, 2 gate/up, 3 down, 4 lm_head; None: not a layer launch); above 32
+    rows the layer launches take 32-row tiles (rows_nt_max 0 = auto) with e4m3 weights or at
+    most 128 rows."""
     if kind is not None and (o["rows_nt1"] >> kind) & 1 and R <= 32:
         return 1
+    if o["rows_nt_max"] == 0 and kind is not None and kind < 4 and R > 32 and (f8 or R <= 128):
+        return 2
     return o["rows_nt_max"]
 
 
 def rows_launch(N, K, R, epi, norm, f8, o, merge_nsm=0, kind=None):
     """launch_gemm_rows_v4 -> the instantiation (None where it returns NotSupported)."""
-    mt, nt = rows_tiles(R, nt_max_of(o, kind, R))
+    mt, nt = rows_tiles(R, nt_max_of(o, kind, R, f8))
     o = target_opts(o, kind)
     if epi == EPI_ARGMAX and norm and o["rows_head_mt"] == 2 and nt in (1, 2):
         mt = 2

@@ -259,6 +259,18 @@ def test_batched_decode_orpheus_width_8_rows_eight_wave_attention():
                                max_prefill=600, options={"att_nw6": 0}) >= 0.8 * 8 * 6
 
 
+def test_prefill_batch_tile_classes_orpheus_width():
+    """Prefill launches above 32 rows (capi.hip nt_cap): 32-row batch tiles up to 128 rows
+    (a 100-id prompt: qkv gemm_rows_kernel<1,2,3,true,24,...>, o-proj <1,2,1,false,12,...>),
+    64-row tiles above (a 150-id prompt: <1,4,3,true,12,...>, <1,4,1,false,6,...>); then the
+    two streams decode together, teacher-forced."""
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=95)
+    rng = np.random.default_rng(96)
+    prompts = [[int(x) for x in rng.integers(0, cfg.vocab, n)] for n in (100, 150)]
+    assert rows_teacher_forced(cfg, w, prompts, 6, max_pos=512, max_prefill=160) >= 0.8 * 2 * 6
+
+
 @pytest.mark.parametrize("case", sorted(STRADDLE))
 def test_rows_merge_straddling_splits_orpheus_width(case):
     """The generation-4 merging o-projection (rows_merge, the default) where the rows of one
