@@ -163,7 +163,7 @@ def rocprof_avg_us(kernel=ROOFLINE_KERNEL):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats*.csv")),
                    key=lambda f: (os.path.basename(f)[:3], "final" in os.path.basename(f),
-                                  os.path.getmtime(f)))
+                                  os.path.basename(f)))
     for path in reversed(files):
         try:
             with open(path) as fh:
