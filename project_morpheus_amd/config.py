@@ -115,12 +115,14 @@ MX_MAX_POS = env_int("MORPHEUS_MX_MAX_POS", env_int("LLAMA_N_CTX", 8192))
 MX_MAX_SLOTS = env_int("MORPHEUS_MX_MAX_SLOTS", 8)
 MX_GPUS = env_int("MORPHEUS_MX_GPUS", 1)                # worker processes (one per GPU)
 # batched SNAC window coalescing (batching.BatchSynthesizer): launch when this many windows
-# are due, or when the oldest has waited SNAC_MAX_HOLD decode steps (12 / 2 measured: configs[2]
-# 96.8 -> 99.2x, p50 first audio +1.4 ms; profiles/r02_bench_snac_coalescing.log)
+# are due, or when the oldest has waited SNAC_MAX_HOLD decode steps (12 / 2 measured in round 2:
+# configs[2] 96.8 -> 99.2x, p50 first audio +1.4 ms; profiles/r02_bench_snac_coalescing.log;
+# 16 / 3 since round 6's receptive-field cut: the configs[2] loop 3.253 -> 3.241 s,
+# profiles/r06_snac_coalescing_sweep.log)
 # decode steps the batcher keeps queued ahead of the host (batching.BatchSynthesizer)
 BATCH_DEPTH = env_int("MORPHEUS_MX_BATCH_DEPTH", 2)
-SNAC_MIN_BATCH = env_int("MORPHEUS_MX_SNAC_MIN_BATCH", 12)
-SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 2)
+SNAC_MIN_BATCH = env_int("MORPHEUS_MX_SNAC_MIN_BATCH", 16)
+SNAC_MAX_HOLD = env_int("MORPHEUS_MX_SNAC_MAX_HOLD", 3)
 # Random streams of a request given no seed (sampling + SNAC noise): 0 (default) draws a fresh
 # 64-bit seed per request, as vLLM SamplingParams(seed=None) and llama.cpp's default do, so
 # "regenerate" gives new audio; 1 derives it from the prompt ids (reproducible bench / parity

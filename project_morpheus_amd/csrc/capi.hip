@@ -1762,13 +1762,15 @@ extern "C" int mx_snac_finalize(mx_snac* s) {
 // Window batch from which the block-tiled conv-GEMM is used.  Its point is sharing each A
 // (weight) fragment across the windows' columns; one window gains nothing from it and the
 // one-wave kernels give small batches 4-8x the blocks (N7_B1 0.41 vs 0.55 ms, N7_B4 0.18 vs
-// 0.23 ms per window; profiles/r02_snac_tiled_timing.log).  12 since the receptive-field cut
-// (5-frame windows: 8 windows 0.069 vs 0.077 ms per window one-wave, 12: 0.0566 vs 0.0557,
-// 16: 0.052 vs 0.043; profiles/r06_snac_tiled_threshold.log).
+// 0.23 ms per window; profiles/r02_snac_tiled_timing.log).  On the receptive-field-cut shapes
+// a lone call of 8 windows runs 10-14 % faster on the one-wave kernels
+// (profiles/r06_snac_tiled_threshold.log), but inside the configs[2] loop, beside the decode
+// stream, the tiled kernel from 8 windows gives the shorter wall (3.245 vs 3.275 s;
+// profiles/r06_snac_coalescing_sweep.log), so 8 stays.
 static int snac_tiled_min_batch() {
   static const int v = [] {
     const char* e = getenv("MORPHEUS_MX_SNAC_TILED_MIN_BATCH");
-    return e ? atoi(e) : 12;
+    return e ? atoi(e) : 8;
   }();
   return v;
 }

@@ -6,7 +6,7 @@ kernels the bench runs can be checked on the CPU (tests/test_snac_coverage.py):
 * ``capi.hip`` ``snac_enqueue`` (the 36 launches of one call, 37 with the receptive-field cut
   of a PCM-only call: embed, input depthwise conv and 1x1 conv, then per DecoderBlock the polyphase ConvTranspose, the NoiseBlock and three
   ResidualUnits, then the output stage) and ``pick_tiles`` (block-tiled kernel from
-  ``snac_tiled_min_batch()`` = 12 windows when M % 64 == 0; otherwise 16 x NSUB column tiles,
+  ``snac_tiled_min_batch()`` = 8 windows when M % 64 == 0; otherwise 16 x NSUB column tiles,
   NSUB = 4 from 2,048 input steps, and WK K-splitting waves doubled while the launch stays
   <= 2,048 waves);
 * ``snac_kernels.hip`` ``launch_conv_gemm`` (WK = 1 -> ``conv_gemm1_kernel<NSUB>``, else
@@ -25,7 +25,7 @@ from __future__ import annotations
 
 K_RATES = (8, 8, 4, 2)
 K_DIL = (1, 3, 9)
-TILED_MIN_BATCH = 12
+TILED_MIN_BATCH = 8
 
 
 def pick_tiles(M, Cin, Tin, B, nseg, nphase, tiled_min=TILED_MIN_BATCH):

@@ -44,11 +44,10 @@ def _split_noise(noise_row, n):
 @pytest.mark.parametrize("n_frames,B", [(1, 1), (4, 1), (7, 1), (7, 3), (2, 2), (1, 5), (4, 9),
                                         (7, 12), (5, 1), (5, 12)])
 def test_snac_window_parity(snac_pair, n_frames, B):
-    """(1, 5): the 2-wave conv-GEMM with a ragged column tile; (4, 9): the one-wave kernels
-    just below the block-tiled threshold (12 windows); (7, 12): the block-tiled conv-GEMM below
-    32 windows, its last 128-column tile cut by the end of the batch and tiles holding columns
-    of two windows (tests/_snac_dispatch.py keys); (5, *): the shape the serving path decodes a
-    7-frame window as (schedule.frames_for_slice)."""
+    """(1, 5): the 2-wave conv-GEMM with a ragged column tile; (4, 9) and (7, 12): the
+    block-tiled conv-GEMM below 32 windows, its last 128-column tile cut by the end of the
+    batch and tiles holding columns of two windows (tests/_snac_dispatch.py keys); (5, *): the
+    shape the serving path decodes a 7-frame window as (schedule.frames_for_slice)."""
     from _coverage import check_declared_snac
     check_declared_snac(n_frames, B)
     w, dec = snac_pair

@@ -72,7 +72,7 @@ def test_pick_tiles_restatement_spot_values():
     phases, K 2 x 1,024: WK 8)."""
     assert S.conv_gemm_key(1024, 768, 28, 1, 1, 1) == "conv_gemm_kernel<4, 2> [ragged]"
     assert S.conv_gemm_key(512, 1024, 28, 1, 2, 8) == "conv_gemm_kernel<8, 2> [ragged]"
-    assert S.conv_gemm_key(1024, 768, 28, 12, 1, 1).startswith("conv_gemm_tiled_kernel<1>")
-    assert not S.conv_gemm_key(1024, 768, 28, 11, 1, 1).startswith("conv_gemm_tiled_kernel<1>")
+    assert S.conv_gemm_key(1024, 768, 28, 8, 1, 1).startswith("conv_gemm_tiled_kernel<1>")
+    assert not S.conv_gemm_key(1024, 768, 28, 7, 1, 1).startswith("conv_gemm_tiled_kernel<1>")
     assert S.dwconv_key(32, 1792) == "dwconv_kernel<64>"
     assert S.dwconv_key(1, 1792) == "dwconv_kernel<16>"
