@@ -127,6 +127,8 @@ struct mx_llm {
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
+  int att_b1_short = 0;                 // option: one-row attention may take 64 / 96-position
+                                        // splits (2: both, 1: 96 only; 0: from 128)
   int att_nw6 = 1;                      // option: multi-row attention may take 6-wave blocks
                                         // (8 rows, L 300-1100: -0.3..-0.7 % per step, bf16 and
                                         // e4m3; profiles/r06_att_nw6_gemv_balance.log)
@@ -607,11 +609,14 @@ static void att_b1_shape(const mx_llm* x, int max_len, int* nw, int* cpw) {
     *cpw = x->att_cpw_b1;
     return;
   }
-  static const int shapes[5][2] = {{4, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
-  for (const auto& sh : shapes) {
-    *nw = sh[0];
-    *cpw = sh[1];
-    if ((max_len + 32 * sh[0] * sh[1] - 1) / (32 * sh[0] * sh[1]) <= 8) return;
+  // option att_b1_short: splits of 64 / 96 positions (2- / 3-wave blocks) first, i.e. more
+  // blocks with fewer KV bytes each, for contexts they cover in <= 8 splits
+  static const int shapes[7][2] = {{2, 1}, {3, 1}, {4, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
+  const int first = x->att_b1_short == 2 ? 0 : x->att_b1_short == 1 ? 1 : 2;
+  for (int i = first; i < 7; ++i) {
+    *nw = shapes[i][0];
+    *cpw = shapes[i][1];
+    if ((max_len + 32 * *nw * *cpw - 1) / (32 * *nw * *cpw) <= 8) return;
   }
 }
 
@@ -757,7 +762,9 @@ static hipError_t enqueue_layers(mx_llm* x, const RowSet& rs, hipStream_t st, Pr
     at.scale = 1.0f / sqrtf(128.0f);
     at.cpw = rs.cpw;
     at.nw = rs.nw;
-    at.split_stride = c.max_pos / ATT_S_MIN;
+    // (splits shorter than ATT_S_MIN, one-row steps only: the row's partial slots then use the
+    // stride of 64-position splits, which one row fits in the buffers sized for max_rows >= 2)
+    at.split_stride = 32 * rs.nw * rs.cpw < ATT_S_MIN ? c.max_pos / 64 : c.max_pos / ATT_S_MIN;
     // O projection + residual; it merges the attention splits itself (no ticket round trip)
     // at one row, and at 2-16 rows when its tiling allows (option rows_merge)
     GemvArgs o{};
@@ -1454,6 +1461,11 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
   } else if (k == "gemv_balance") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "gemv_balance must be 0 or 1");
     x->gemv_balance = value;
+  } else if (k == "att_b1_short") {
+    if (value < 0 || value > 2) MX_FAIL(x, MX_ERR_ARG, "att_b1_short must be 0, 1 or 2");
+    if (value && (x->c.max_pos % 64 || x->max_rows < 2))
+      MX_FAIL(x, MX_ERR_ARG, "att_b1_short needs max_pos % 64 == 0 and max(max_batch, max_prefill) >= 2");
+    x->att_b1_short = value;
   } else if (k == "att_nw6") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "att_nw6 must be 0 or 1");
     x->att_nw6 = value;

@@ -40,6 +40,8 @@ GPU_RUNS = {
         [_r(ORPHEUS, [18], 12, o_merge=0)],
     **{f"test_gpu_llm.py::test_decode_parity_orpheus_width_no_gemv_balance[{p}]":
        [_r(ORPHEUS_16K, [p], 16, gemv_balance=0)] for p in (200, 300, 600)},
+    **{f"test_gpu_llm.py::test_decode_parity_orpheus_width_short_splits[{p}]":
+       [_r(ORPHEUS_16K, [p], 16, att_b1_short=2)] for p in (200, 600)},
     "test_gpu_llm.py::test_lm_head_grid_stride_orpheus_width":
         [_r(ORPHEUS, [24], 16, head_b1=0)],
     "test_gpu_llm.py::test_full_depth_orpheus_3b_single_stream":

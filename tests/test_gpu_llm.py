@@ -326,6 +326,23 @@ def test_decode_parity_orpheus_width_no_gemv_balance(prompt_len):
                     max_prefill=prompt_len) >= 12
 
 
+@pytest.mark.parametrize("prompt_len", [200, 600])
+def test_decode_parity_orpheus_width_short_splits(prompt_len):
+    """Option att_b1_short = 2: the one-row attention on 64-position splits (2-wave blocks,
+    attn_kernel<3,1,2>) up to 512 positions, 96-position splits (3-wave, <3,1,3>) above, each
+    row's partials at the 64-position stride, merged by the o-proj (NSM 4 / 8), 16 steps."""
+    from _dispatch import ORPHEUS_16K, att_shape, DEFAULTS
+    o = dict(DEFAULTS, att_b1_short=2)
+    assert {att_shape(ORPHEUS_16K, 1, prompt_len + k, o)[0] for k in range(1, 17)} == \
+        ({2} if prompt_len == 200 else {3})
+    cfg = C.OrpheusConfig(layers=2, vocab=16384)
+    w = synthetic_llm_weights(cfg, seed=97 + prompt_len)
+    rng = np.random.default_rng(98)
+    prompt = [int(x) for x in rng.integers(0, cfg.vocab, prompt_len)]
+    assert _compare(cfg, w, prompt, 16, options={"att_b1_short": 2}, max_pos=1024,
+                    max_prefill=prompt_len) >= 12
+
+
 def test_lm_head_grid_stride_orpheus_width():
     """The one-row lm_head's other kernel (option head_b1 = 0: the grid-stride gemv_kernel
     that stages the row per block; the default is the persistent head_b1.hip), full
