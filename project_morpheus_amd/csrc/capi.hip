@@ -127,8 +127,10 @@ struct mx_llm {
   int att_cpw_batch = 0;        // option: same for multi-row (batched decode / prefill); 0 =
                                 // auto (att_cpw_auto): measured -14 % attention at 32 rows
   int att_nw_b1 = 4, att_nw_batch = 8;  // options: attention waves per block (4 or 8; measured)
-  int att_b1_short = 0;                 // option: one-row attention may take 64 / 96-position
-                                        // splits (2: both, 1: 96 only; 0: from 128)
+  int att_b1_short = 1;                 // option: one-row attention may take 64 / 96-position
+                                        // splits (2: both, 1: 96 only; 0: from 128). 1 measured
+                                        // -1.8 % bf16 / -2.6 % e4m3 per step at L 600, 2 slower
+                                        // at L 300 (profiles/r06_att_b1_short.log)
   int att_nw6 = 1;                      // option: multi-row attention may take 6-wave blocks
                                         // (8 rows, L 300-1100: -0.3..-0.7 % per step, bf16 and
                                         // e4m3; profiles/r06_att_nw6_gemv_balance.log)
@@ -612,7 +614,8 @@ static void att_b1_shape(const mx_llm* x, int max_len, int* nw, int* cpw) {
   // option att_b1_short: splits of 64 / 96 positions (2- / 3-wave blocks) first, i.e. more
   // blocks with fewer KV bytes each, for contexts they cover in <= 8 splits
   static const int shapes[7][2] = {{2, 1}, {3, 1}, {4, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
-  const int first = x->att_b1_short == 2 ? 0 : x->att_b1_short == 1 ? 1 : 2;
+  const bool fits = x->c.max_pos % 64 == 0 && x->max_rows >= 2;  // (the 64-position stride)
+  const int first = !fits ? 2 : x->att_b1_short == 2 ? 0 : x->att_b1_short == 1 ? 1 : 2;
   for (int i = first; i < 7; ++i) {
     *nw = shapes[i][0];
     *cpw = shapes[i][1];

@@ -49,7 +49,7 @@ GPU_RUNS = {
     "test_gpu_llm.py::test_long_context_orpheus_width_default_path":
         [_r(ORPHEUS_16K, [600], 520)],
     "test_gpu_llm.py::test_one_row_orpheus_width_split_classes":
-        [_r(ORPHEUS_16K, [250], 16)],
+        [_r(ORPHEUS_16K, [185], 16)],
     "test_gpu_llm.py::test_long_context_orpheus_width_past_2048_4096[2048]":
         [_r(ORPHEUS_16K, [2040], 16)],
     "test_gpu_llm.py::test_long_context_orpheus_width_past_2048_4096[4096]":
@@ -103,7 +103,7 @@ GPU_RUNS = {
     "test_gpu_fp8.py::test_fp8_single_stream_orpheus_width_long_context":
         [_r(ORPHEUS_16K, [600], 520, f8=True)],
     "test_gpu_fp8.py::test_fp8_one_row_orpheus_width_split_classes":
-        [_r(ORPHEUS_16K, [250], 16, f8=True)],
+        [_r(ORPHEUS_16K, [185], 16, f8=True)],
     "test_gpu_fp8.py::test_fp8_rows_merge_straddling_splits_orpheus_width[nsm2]":
         [_r(ORPHEUS_16K, [200, 215, 230, 250, 262, 280, 400, 497], 12, f8=True, att_nw6=0)],
     "test_gpu_fp8.py::test_fp8_rows_merge_straddling_splits_orpheus_width[nsm4]":

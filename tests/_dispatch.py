@@ -47,7 +47,7 @@ DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
                 rows_nt_max=0, rows_nt1=2, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
                 rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7, rows_atomic=1,
-                rows_qkv_parts=1, att_nw6=1, gemv_balance=1, att_b1_short=0)
+                rows_qkv_parts=1, att_nw6=1, gemv_balance=1, att_b1_short=1)
 # (rows_atomic and rows_qkv_parts select the residual projections' split-K epilogue at run time inside the same
 # instantiation -- float atomics into h / raw partials summed by the attention, or the
 # seam -- so they change no kernel key)

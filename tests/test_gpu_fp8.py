@@ -174,12 +174,12 @@ def test_fp8_single_stream_orpheus_width_long_context():
 
 
 def test_fp8_one_row_orpheus_width_split_classes():
-    """The e4m3 one-row merging o-proj at NSM 2 and 4 (gemv1<3,2,1,false,8,true,2|4>): a
-    250-id prompt, L 251..265 crosses 2 -> 3 attention splits of 128 positions."""
+    """The e4m3 one-row merging o-proj at NSM 2 and 4 (gemv1<3,2,1,false,6,true,2|4>): a
+    185-id prompt, L 186..200 crosses 2 -> 3 attention splits of 96 positions."""
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     qw = quantize_fp8(synthetic_llm_weights(cfg, seed=79), cfg)
-    prompt = [int(x) for x in np.random.default_rng(80).integers(0, cfg.vocab, 250)]
-    assert b1_attention_shapes(251, 265) == {(4, 1, 2), (4, 1, 3)}
+    prompt = [int(x) for x in np.random.default_rng(80).integers(0, cfg.vocab, 185)]
+    assert b1_attention_shapes(186, 200) == {(3, 1, 2), (3, 1, 3)}
     assert _check(cfg, qw, [prompt], 16, max_pos=512, max_prefill=256) >= 12
 
 

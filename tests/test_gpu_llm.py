@@ -138,13 +138,13 @@ def test_long_context_orpheus_width_default_path():
 
 
 def test_one_row_orpheus_width_split_classes():
-    """The one-row merging o-proj at NSM 2 and 4 at Orpheus widths (gemv1<6,2,1,false,8,
-    false,2|4>): a 250-id prompt, L 251..265 crosses 256, i.e. 2 -> 3 attention splits of
-    128 positions."""
+    """The one-row merging o-proj at NSM 2 and 4 at Orpheus widths (gemv1<6,2,1,false,6,
+    false,2|4>): a 185-id prompt, L 186..200 crosses 192, i.e. 2 -> 3 attention splits of
+    96 positions."""
     cfg = C.OrpheusConfig(layers=2, vocab=16384)
     w = synthetic_llm_weights(cfg, seed=73)
-    prompt = [int(x) for x in np.random.default_rng(74).integers(0, cfg.vocab, 250)]
-    assert b1_attention_shapes(251, 265) == {(4, 1, 2), (4, 1, 3)}
+    prompt = [int(x) for x in np.random.default_rng(74).integers(0, cfg.vocab, 185)]
+    assert b1_attention_shapes(186, 200) == {(3, 1, 2), (3, 1, 3)}
     assert _compare(cfg, w, prompt, 16, max_pos=512, max_prefill=256) >= 12
 
 
