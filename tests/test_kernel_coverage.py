@@ -29,7 +29,8 @@ BENCH_TRACES = [("profiles/r04_bench_kernel_stats_final.csv", {"rows_head_mt": 2
                 ("profiles/r06_bench_kernel_stats_v1.csv", dict(_R06)),
                 ("profiles/r06_bench_kernel_stats_final.csv", {"rows_nt_max": 4, "att_b1_short": 0}),
                 ("profiles/r06_bench_kernel_stats_final2.csv", {"att_b1_short": 0}),
-                ("profiles/r06_bench_kernel_stats_final3.csv", {"att_b1_short": 0})]
+                ("profiles/r06_bench_kernel_stats_final3.csv", {"att_b1_short": 0}),
+                ("profiles/r06_bench_kernel_stats_final4.csv", {})]
 _LLM = re.compile(r"void mx::((?:v4::gemm_rows|attn|gemv1?|head1::head_b1)_kernel<[^>]*>)"
                   r"\((?:mx::GemvArgs|mx::AttnArgs)\)")
 
