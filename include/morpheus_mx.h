@@ -110,7 +110,8 @@ int mx_llm_decode_profiled(mx_llm* ctx, int n_rows, void* stream, double* ms_by_
 /* Tuning knobs (capi.hip mx_llm_set_option; unknown keys and out-of-range values fail with
  * MX_ERR_ARG): "legacy_gemv", "gemv_wpb", "rpw_o", "rpw_gu", "rpw_down", "head_b1",
  * "o_merge", "att_cpw", "att_nw", "att_cpw_batch", "att_nw_batch", "att_b1_short" (one-row
- * attention may split the context into 64- / 96-position pieces: 2 / 1), "att_nw6" (multi-row
+ * attention may split the context into 64- / 96-position pieces: 2 / 1), "att_b1_nw6" (one-row
+ * attention may take 192-position splits on 6-wave blocks past L 1,024), "att_nw6" (multi-row
  * attention may pick 6-wave blocks: the shortest split covering the context), "gemv_balance"
  * (one-row qkv / merging o-proj: the waves per block that load the most loaded CU least), "rows_frag",
  * "rows_merge", "rows_head_mt", "rows_head_target", "rows_target", "rows_target_qkv", "rows_target_o",

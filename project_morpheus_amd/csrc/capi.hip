@@ -131,6 +131,9 @@ struct mx_llm {
                                         // splits (2: both, 1: 96 only; 0: from 128). 1 measured
                                         // -1.8 % bf16 / -2.6 % e4m3 per step at L 600, 2 slower
                                         // at L 300 (profiles/r06_att_b1_short.log)
+  int att_b1_nw6 = 1;                   // option: one-row attention may take 192-position
+                                        // splits (6-wave blocks) past L 1,024: measured -0.6 to
+                                        // -0.8 % bf16, -1.1 % e4m3 per step at L 1,100..1,400
   int att_nw6 = 1;                      // option: multi-row attention may take 6-wave blocks
                                         // (8 rows, L 300-1100: -0.3..-0.7 % per step, bf16 and
                                         // e4m3; profiles/r06_att_nw6_gemv_balance.log)
@@ -613,10 +616,13 @@ static void att_b1_shape(const mx_llm* x, int max_len, int* nw, int* cpw) {
   }
   // option att_b1_short: splits of 64 / 96 positions (2- / 3-wave blocks) first, i.e. more
   // blocks with fewer KV bytes each, for contexts they cover in <= 8 splits
-  static const int shapes[7][2] = {{2, 1}, {3, 1}, {4, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
+  // option att_b1_nw6: 192-position splits (6-wave blocks) between 128 and 256, i.e. 6..8
+  // splits at L 1,025..1,536 instead of 5..6 of 256 (profiles/r06_att_b1_nw6.log)
+  static const int shapes[8][2] = {{2, 1}, {3, 1}, {4, 1}, {6, 1}, {4, 2}, {4, 4}, {8, 4}, {8, 8}};
   const bool fits = x->c.max_pos % 64 == 0 && x->max_rows >= 2;  // (the 64-position stride)
   const int first = !fits ? 2 : x->att_b1_short == 2 ? 0 : x->att_b1_short == 1 ? 1 : 2;
-  for (int i = first; i < 7; ++i) {
+  for (int i = first; i < 8; ++i) {
+    if (i == 3 && !x->att_b1_nw6) continue;
     *nw = shapes[i][0];
     *cpw = shapes[i][1];
     if ((max_len + 32 * *nw * *cpw - 1) / (32 * *nw * *cpw) <= 8) return;
@@ -1469,11 +1475,16 @@ extern "C" int mx_llm_set_option(mx_llm* x, const char* key, int value) {
     if (value && (x->c.max_pos % 64 || x->max_rows < 2))
       MX_FAIL(x, MX_ERR_ARG, "att_b1_short needs max_pos % 64 == 0 and max(max_batch, max_prefill) >= 2");
     x->att_b1_short = value;
+  } else if (k == "att_b1_nw6") {
+    if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "att_b1_nw6 must be 0 or 1");
+    x->att_b1_nw6 = value;
   } else if (k == "att_nw6") {
     if (value != 0 && value != 1) MX_FAIL(x, MX_ERR_ARG, "att_nw6 must be 0 or 1");
     x->att_nw6 = value;
   } else if (k == "att_nw" || k == "att_nw_batch") {
-    if (value != 4 && value != 8) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8");
+    // (one-row overrides with att_cpw > 0 may also take 3- / 6-wave blocks)
+    const bool b1_only = (value == 3 || value == 6) && k == "att_nw";
+    if (value != 4 && value != 8 && !b1_only) MX_FAIL(x, MX_ERR_ARG, "att_nw must be 4 or 8 (att_nw also 3 / 6)");
     (k == "att_nw" ? x->att_nw_b1 : x->att_nw_batch) = value;
   } else if (k == "rows_pw" || k == "rows_pw_f8") {
     if (value < 1 || value > 2) MX_FAIL(x, MX_ERR_ARG, "rows_pw / rows_pw_f8 must be 1 or 2");

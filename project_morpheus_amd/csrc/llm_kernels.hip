@@ -1175,7 +1175,7 @@ hipError_t launch_attention(const AttnArgs& a, int R, int max_len, hipStream_t s
     hipLaunchKernelGGL((attn_kernel<G_, C_, W_>), grid, dim3(64 * W_), 0, st, a);    \
     return hipGetLastError();                                                        \
   }
-#define MX_ATG(G_) MX_AT(G_, 1, 2) MX_AT(G_, 1, 3) MX_AT(G_, 1, 4) MX_AT(G_, 2, 4) MX_AT(G_, 4, 4) \
+#define MX_ATG(G_) MX_AT(G_, 1, 2) MX_AT(G_, 1, 3) MX_AT(G_, 2, 3) MX_AT(G_, 1, 4) MX_AT(G_, 2, 4) MX_AT(G_, 4, 4) \
                    MX_AT(G_, 1, 6) MX_AT(G_, 2, 6) MX_AT(G_, 3, 6) \
                    MX_AT(G_, 1, 8) MX_AT(G_, 2, 8) MX_AT(G_, 3, 8) MX_AT(G_, 4, 8) \
                    MX_AT(G_, 6, 8) MX_AT(G_, 8, 8)

@@ -19,13 +19,17 @@ DEFAULTS = {"legacy_gemv": 0, "att_cpw": 0, "att_cpw_batch": 0, "att_nw": 4, "at
             "o_merge": 1, "rows_frag": 1, "rows_target": 0, "rows_pw": 2, "rows_pw_f8": 2,
             "rows_head_mt": 1, "rows_head_target": 0, "rows_nt_max": 0, "rows_nt1": 2, "head_b1": 1, "rows_merge": 1, "engine_slots": 7, "engine_depth": 2, "engine_loaders": 2, "b1_engine": 0, "rows_atomic": 1, "rows_qkv_parts": 1,
             "rows_target_qkv": 0, "rows_target_o": 0, "rows_target_gu": 0, "rows_target_down": 0,
-            "att_nw6": 1, "gemv_balance": 1, "att_b1_short": 1}
+            "att_nw6": 1, "gemv_balance": 1, "att_b1_short": 1, "att_b1_nw6": 1}
 VARIANTS = {
     "base": {},
     "no_nw6": {"att_nw6": 0},
     "short0": {"att_b1_short": 0},
     "short2": {"att_b1_short": 2},
     "no_balance": {"gemv_balance": 0},
+    "no_b1_nw6": {"att_b1_nw6": 0},
+    "b1_61": {"att_cpw": 1, "att_nw": 6},
+    "b1_32": {"att_cpw": 2, "att_nw": 3},
+    "b1_81": {"att_cpw": 1, "att_nw": 8},
     "ticket": {"o_merge": 0, "att_cpw": 1},
     "rpw_o2": {"rpw_o": 2},
     "cpw2": {"att_cpw": 2},

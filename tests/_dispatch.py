@@ -47,7 +47,8 @@ DEFAULTS = dict(att_cpw=0, att_nw=4, att_nw_batch=8, att_cpw_batch=0, o_merge=1,
                 rows_merge=1, gemv_wpb=4, rows_pw=2, rows_pw_f8=2, rows_target=0,
                 rows_nt_max=0, rows_nt1=2, rows_head_target=0, rows_head_mt=1, head_b1=1, rpw_o=0,
                 rpw_gu=0, rpw_down=0, legacy_gemv=0, b1_engine=0, engine_slots=7, rows_atomic=1,
-                rows_qkv_parts=1, att_nw6=1, gemv_balance=1, att_b1_short=1)
+                rows_qkv_parts=1, att_nw6=1, gemv_balance=1, att_b1_short=1,
+                att_b1_nw6=1)
 # (rows_atomic and rows_qkv_parts select the residual projections' split-K epilogue at run time inside the same
 # instantiation -- float atomics into h / raw partials summed by the attention, or the
 # seam -- so they change no kernel key)
@@ -61,9 +62,11 @@ def _b(v):
 def att_b1_shape(max_len, o):
     if o["att_cpw"] > 0:
         return o["att_nw"], o["att_cpw"]
-    shapes = ((2, 1), (3, 1), (4, 1), (4, 2), (4, 4), (8, 4), (8, 8))
+    shapes = ((2, 1), (3, 1), (4, 1), (6, 1), (4, 2), (4, 4), (8, 4), (8, 8))
     first = {2: 0, 1: 1}.get(o.get("att_b1_short", 0), 2)
     for nw, cpw in shapes[first:]:
+        if (nw, cpw) == (6, 1) and not o.get("att_b1_nw6", 0):
+            continue
         if (max_len + 32 * nw * cpw - 1) // (32 * nw * cpw) <= 8:
             return nw, cpw
     return 8, 8

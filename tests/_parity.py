@@ -31,8 +31,8 @@ def b1_attention_shapes(l_lo, l_hi):
     l_lo..l_hi -- a restatement of capi.hip att_b1_shape, so the long-context tests can
     assert which kernel variants they reached."""
     out = set()
-    for L_ in range(l_lo, l_hi + 1):  # (option att_b1_short = 1, the default: 96 positions first)
-        for nw, cpw in ((3, 1), (4, 1), (4, 2), (4, 4), (8, 4), (8, 8)):
+    for L_ in range(l_lo, l_hi + 1):  # (options att_b1_short = 1, att_b1_nw6 = 1, the defaults)
+        for nw, cpw in ((3, 1), (4, 1), (6, 1), (4, 2), (4, 4), (8, 4), (8, 8)):
             S = 32 * nw * cpw
             if (L_ + S - 1) // S <= 8:
                 out.add((nw, cpw, (L_ + S - 1) // S))
@@ -41,8 +41,8 @@ def b1_attention_shapes(l_lo, l_hi):
 
 
 # the default one-row shapes configs[1] reaches past L 600: 7..8 splits of 96 positions to
-# L 768, 7..8 of 128 to 1,024 (the o-proj's NSM = 8 split merge), then 5 splits of 256
-LONG_SHAPES = {(3, 1, 7), (3, 1, 8), (4, 1, 7), (4, 1, 8), (4, 2, 5)}
+# L 768, 7..8 of 128 to 1,024 (the o-proj's NSM = 8 split merge), then 6 splits of 192
+LONG_SHAPES = {(3, 1, 7), (3, 1, 8), (4, 1, 7), (4, 1, 8), (6, 1, 6)}
 
 
 # 8 rows whose own split counts differ inside one launch: the o-projection merging

@@ -114,8 +114,8 @@ def test_long_context_many_splits_small():
 def test_long_context_1250_small():
     """configs[1]'s own context range (prompt + max_tokens 1,200, engine_class.py:103) on the
     default B = 1 path: L 240 -> 1,250 crosses 2..8 attention splits of 128 positions (the
-    o-proj's NSM = 2 / 4 / 8 split merges) and, past 1,024, the 256-position
-    attn_kernel<G,2,4> with 5 splits."""
+    o-proj's NSM = 2 / 4 / 8 split merges) and, past 1,024, the 192-position
+    attn_kernel<G,1,6> with 6..7 splits (option att_b1_nw6)."""
     cfg = _cfgs("small")
     w = synthetic_llm_weights(cfg, seed=14, std=0.05, norm_jitter=0.5)
     prompt = [int(x) for x in np.random.default_rng(5).integers(0, cfg.vocab, 240)]
@@ -126,7 +126,7 @@ def test_long_context_1250_small():
 def test_long_context_orpheus_width_default_path():
     """The exact one-row kernel instantiations configs[1] runs at L 600..1,120 (Orpheus widths:
     the KCH = 6 merging o-proj gemv1<6,2,1,false,8,false,NSM> at 5..8 splits, then
-    attn_kernel<3,2,4> past 1,024), teacher-forced.  Two layers and a 16,384-entry vocabulary
+    attn_kernel<3,1,6> past 1,024), teacher-forced.  Two layers and a 16,384-entry vocabulary
     keep the CPU oracle to seconds per hundred steps (the lm_head GEMV instantiation depends
     on the hidden width, not on the vocabulary size)."""
     cfg = C.OrpheusConfig(layers=2, vocab=16384)

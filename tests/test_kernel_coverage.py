@@ -21,16 +21,16 @@ from _dispatch import PREFILL_TAG
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # rocprofv3 --kernel-trace --stats of whole default bench runs (scripts/gpu_full.sh), with the
 # options whose default has changed since the trace was recorded
-_R06 = {"att_nw6": 0, "gemv_balance": 0, "rows_nt_max": 4, "att_b1_short": 0}  # defaults before round 6's last changes
+_R06 = {"att_nw6": 0, "gemv_balance": 0, "rows_nt_max": 4, "att_b1_short": 0, "att_b1_nw6": 0}  # defaults before round 6's last changes
 BENCH_TRACES = [("profiles/r04_bench_kernel_stats_final.csv", {"rows_head_mt": 2, "rows_nt1": 0, **_R06}),
                 ("profiles/r05_bench_kernel_stats.csv", {"rows_head_mt": 2, "rows_nt1": 0, **_R06}),
                 ("profiles/r05_bench_kernel_stats_check2.csv", {"rows_nt1": 0, **_R06}),
                 ("profiles/r05_bench_kernel_stats_final.csv", {"rows_nt1": 11, **_R06}),
                 ("profiles/r06_bench_kernel_stats_v1.csv", dict(_R06)),
-                ("profiles/r06_bench_kernel_stats_final.csv", {"rows_nt_max": 4, "att_b1_short": 0}),
-                ("profiles/r06_bench_kernel_stats_final2.csv", {"att_b1_short": 0}),
-                ("profiles/r06_bench_kernel_stats_final3.csv", {"att_b1_short": 0}),
-                ("profiles/r06_bench_kernel_stats_final4.csv", {})]
+                ("profiles/r06_bench_kernel_stats_final.csv", {"rows_nt_max": 4, "att_b1_short": 0, "att_b1_nw6": 0}),
+                ("profiles/r06_bench_kernel_stats_final2.csv", {"att_b1_short": 0, "att_b1_nw6": 0}),
+                ("profiles/r06_bench_kernel_stats_final3.csv", {"att_b1_short": 0, "att_b1_nw6": 0}),
+                ("profiles/r06_bench_kernel_stats_final4.csv", {"att_b1_nw6": 0})]
 _LLM = re.compile(r"void mx::((?:v4::gemm_rows|attn|gemv1?|head1::head_b1)_kernel<[^>]*>)"
                   r"\((?:mx::GemvArgs|mx::AttnArgs)\)")
 
